@@ -1,0 +1,213 @@
+"""Benchmark: DPEngine.aggregate COUNT+SUM+PRIVACY_ID_COUNT on MI355X.
+
+Workload = BASELINE.json configs[1] per GPU: 1e9 records, 1e7 privacy ids,
+1e6 Zipf(1.1) partitions (fixed permutation seeded 20250202), values
+U[0, 10), mpc = 8, mcpp = 2 (bounding triggers), Laplace noise, eps = 1,
+delta = 1e-6, truncated-geometric private partition selection.  With N GPUs
+every rank holds its own privacy-id shard of the same size (weak scaling,
+configs[2]); the partials are merged with one RCCL reduce-scatter.
+
+A step = one full DPEngine.aggregate call on resident inputs: engine +
+accountant construction, aggregate(), compute_budgets(), device execution
+(bounding, merge, selection, noise, compaction) and the device sync.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--records R]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "records/sec DPEngine.aggregate COUNT+SUM at 1/2/4/8 MI355X; % HBM roofline"
+HBM_PEAK_GBS = 8000.0
+ALGO_BYTES_PER_RECORD = 24  # pid int64 + pk int64 + value f64
+
+
+def zipf_cdf(P: int, s: float, device) -> torch.Tensor:
+    w = torch.arange(1, P + 1, dtype=torch.float64, device=device).pow(-s)
+    c = torch.cumsum(w, 0)
+    return c / c[-1]
+
+
+def generate(n: int, n_pid: int, P: int, rank: int, seed: int, device):
+    """Synthetic Zipf-keyed records generated on the device (untimed)."""
+    gen = torch.Generator(device=device)
+    gen.manual_seed(seed * 1000 + rank)
+    cdf = zipf_cdf(P, 1.1, device)
+    perm = torch.randperm(P, generator=torch.Generator().manual_seed(20250202)).to(device)
+    pid = torch.empty(n, dtype=torch.int64, device=device)
+    pk = torch.empty(n, dtype=torch.int64, device=device)
+    val = torch.empty(n, dtype=torch.float64, device=device)
+    chunk = 1 << 27
+    for s in range(0, n, chunk):
+        e = min(n, s + chunk)
+        pid[s:e] = torch.randint(0, n_pid, (e - s,), generator=gen, device=device) + rank * n_pid
+        u = torch.rand(e - s, dtype=torch.float64, generator=gen, device=device)
+        r = torch.searchsorted(cdf, u).clamp_(max=P - 1)
+        pk[s:e] = perm[r]
+        val[s:e] = torch.rand(e - s, dtype=torch.float64, generator=gen, device=device) * 10.0
+    return pid, pk, val
+
+
+def host_sample(n: int, n_pid: int, P: int, seed: int):
+    rng = np.random.default_rng(seed)
+    w = np.arange(1, P + 1, dtype=np.float64) ** -1.1
+    cdf = np.cumsum(w)
+    cdf /= cdf[-1]
+    perm = np.random.default_rng(20250202).permutation(P)
+    pid = rng.integers(0, n_pid, n)
+    pk = perm[np.minimum(np.searchsorted(cdf, rng.random(n)), P - 1)]
+    val = rng.random(n) * 10.0
+    return pid, pk, val
+
+
+def cpu_baseline(args, P):
+    """The C oracle (single core) on a bounded sample of the same workload."""
+    from oracle import oracle
+    import pipelinedp_amd as pdp
+    from pipelinedp_amd import combiners
+    n = args.cpu_records
+    n_pid = max(1, int(round(args.pids * n / args.records)))
+    pid, pk, val = host_sample(n, n_pid, P, 99)
+    acc = pdp.NaiveBudgetAccountant(1.0, 1e-6)
+    plan = combiners.CompoundPlan(make_params(args), acc)
+    fields = plan.bound_fields(P)
+    t0 = time.perf_counter()
+    oracle.bound_aggregate(pid, pk, val, fields, 5)
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "records/s", "cores": 1, "kind": "port",
+            "sample": f"{n} records, {n_pid} privacy ids, {P} partitions, same generator; "
+                      f"C oracle bounding+merge only (selection/noise excluded), "
+                      f"{dt:.1f} s on one host core"}
+
+
+def make_params(args):
+    import pipelinedp_amd as pdp
+    return pdp.AggregateParams(
+        metrics=[pdp.Metrics.COUNT, pdp.Metrics.SUM, pdp.Metrics.PRIVACY_ID_COUNT],
+        noise_kind=pdp.NoiseKind.LAPLACE, max_partitions_contributed=args.mpc,
+        max_contributions_per_partition=args.mcpp, min_value=0.0, max_value=10.0)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--records", type=int, default=1_000_000_000)
+    ap.add_argument("--pids", type=int, default=10_000_000)
+    ap.add_argument("--partitions", type=int, default=1_000_000)
+    ap.add_argument("--mpc", type=int, default=8)
+    ap.add_argument("--mcpp", type=int, default=2)
+    ap.add_argument("--cpu-records", type=int, default=4_000_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import pipelinedp_amd as pdp
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    group = None
+    if world > 1:
+        torch.distributed.init_process_group("nccl", device_id=dev)
+        group = torch.distributed.group.WORLD
+    P = args.partitions
+    pid, pk, val = generate(args.records, args.pids, P, rank, 1, dev)
+    torch.cuda.synchronize()
+    backend = pdp.MI355XBackend(device=local, seed=0xD1FF5EED, process_group=group)
+    cols = pdp.ColumnarData(pid=pid, pk=pk, value=val, n_partitions=P)
+    ex = pdp.DataExtractors("pid", "pk", "value")
+    params = make_params(args)
+
+    def step():
+        acc = pdp.NaiveBudgetAccountant(1.0, 1e-6)
+        eng = pdp.DPEngine(acc, backend)
+        res = eng.aggregate(cols, params, ex)
+        acc.compute_budgets()
+        out = res.materialize(gather=False)
+        return res, out
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if group is not None:
+        torch.distributed.barrier()
+    # device time of the hot path (HIP events on the stream the kernels use)
+    stream = torch.cuda.current_stream(dev)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    stage_tot = {}
+    ev0.record(stream)
+    kept = 0
+    for _ in range(args.steps):
+        res, out = step()
+        kept = int(out.partition_ids.numel())
+        for k, v in backend.ctx.stage_times().items():
+            stage_tot[k] = stage_tot.get(k, 0.0) + v
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if group is not None:
+        torch.distributed.barrier()
+    wall = time.perf_counter() - t0
+    dev_ms = ev0.elapsed_time(ev1) / args.steps
+    t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    if group is not None:
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    wall = float(t.item())
+    ms_per_step = wall / args.steps * 1e3
+    total_records = args.records * world
+    value = total_records / (wall / args.steps)
+    stage_ms = {k: v / args.steps for k, v in stage_tot.items()}
+    bound_ms = sum(stage_ms.values())
+    achieved = ALGO_BYTES_PER_RECORD * args.records / (bound_ms * 1e-3) / 1e9 if bound_ms else None
+    traffic = None
+    tfile = os.path.join(ROOT, "profiles", "hbm_traffic.json")
+    if os.path.exists(tfile):
+        try:
+            tj = json.load(open(tfile))
+            if tj.get("records") == args.records:
+                traffic = tj.get("bytes_per_step")
+        except Exception:
+            traffic = None
+    line = {
+        "metric": METRIC, "value": value, "unit": "records/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f64", "data": "synthetic (device-generated Zipf keys, uniform values)",
+        "config": {"workload": "configs[1]: 1e9 records / 1e7 privacy ids / 1e6 Zipf(1.1) "
+                               "partitions per GPU, COUNT+SUM+PRIVACY_ID_COUNT, private "
+                               "partition selection",
+                   "records_per_gpu": args.records, "privacy_ids_per_gpu": args.pids,
+                   "partitions": P, "max_partitions_contributed": args.mpc,
+                   "max_contributions_per_partition": args.mcpp, "noise": "laplace",
+                   "epsilon": 1.0, "delta": 1e-6,
+                   "selection": "truncated_geometric", "parallelism": f"pid-sharded x{world}"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+                     "traffic": traffic,
+                     "note": "achieved = 24 B/record x records / device time of "
+                             "dpg_bound_aggregate (HIP events per stage, summed)"},
+        "device_ms_per_step": dev_ms, "bound_aggregate_ms": bound_ms, "stage_ms": stage_ms,
+        "kept_partitions": kept,
+    }
+    if rank == 0 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(args, P)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if group is not None:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,195 @@
+/*
+ * dpg.h -- C ABI of the MI355X-native DPEngine.aggregate hot path
+ *          (libdpg.so, built from the HIP sources in pipelinedp_amd/csrc for gfx950).
+ *
+ * Plain pointers and sizes only; no torch or HIP types in the signatures
+ * (streams travel as void*).  Every entry point returns an int status
+ * (DPG_OK = 0) and never throws across the ABI; dpg_last_error() returns
+ * the message of the last failure on a context.  One context per
+ * (host thread, device); calls on one context are not re-entrant.
+ *
+ * Reference interfaces each entry point replaces (paths relative to the
+ * PipelineDP reference tree):
+ *   dpg_bound_aggregate  <- DPEngine._aggregate up to the partition merge:
+ *        pipeline_dp/dp_engine.py:113-151 (extract, drop public, bound,
+ *        drop pid, add empty public, combine_accumulators_per_key), i.e.
+ *        contribution_bounders.py:66-195 + combiners.py:691-706 +
+ *        pipeline_backend.py:531-565 (LocalBackend sample/group/reduce).
+ *   dpg_select_and_noise <- DPEngine._select_private_partitions_internal
+ *        (dp_engine.py:305-361, PyDP create_partition_strategy().should_keep)
+ *        fused with CompoundCombiner.compute_metrics (combiners.py:708-730,
+ *        dp_computations.py:120-184, 307-366, 541-576; PyDP add_noise).
+ *   dpg_compact_kept     <- the LocalBackend `filter` materialisation
+ *        (pipeline_backend.py:514-515) of the selected partitions.
+ */
+#ifndef DPG_H_
+#define DPG_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---- */
+#define DPG_OK 0
+#define DPG_ERR_INVALID_ARG 1
+#define DPG_ERR_KEY_RANGE 2   /* pid outside [0, 2^32) or pk outside [0, P) */
+#define DPG_ERR_HIP 3
+#define DPG_ERR_OOM 4
+#define DPG_ERR_UNSUPPORTED 5
+
+/* ---- Philox key tags: domain separation of the keyed random streams ---- */
+#define DPG_TAG_PAIR 0x50414952u   /* pair priority      (pid, pk)              */
+#define DPG_TAG_REC 0x52454344u    /* record priority    (pid, pk, value, occ)  */
+#define DPG_TAG_SELECT 0x53454C45u /* partition selection (pk)                  */
+#define DPG_TAG_NOISE 0x4E4F4953u  /* metric noise        (pk, slot)            */
+
+/* ---- contribution-bounding modes (dp_engine.py:370-382) ---- */
+#define DPG_MODE_CROSS_AND_PER_PARTITION 0 /* SamplingCrossAndPerPartition   */
+#define DPG_MODE_PER_PRIVACY_ID 1          /* SamplingPerPrivacyId (L1)      */
+#define DPG_MODE_CROSS_PARTITION 2         /* SamplingCrossPartition         */
+
+/* ---- how SUM is bounded (combiners.py:348-353) ---- */
+#define DPG_SUM_NONE 0
+#define DPG_SUM_CLIP_VALUE 1     /* clip every value to [min_value, max_value] */
+#define DPG_SUM_CLIP_PARTITION 2 /* clip the per-(pid,pk) sum                   */
+
+/* ---- accumulator mask ---- */
+#define DPG_M_COUNT 1u
+#define DPG_M_SUM 2u
+#define DPG_M_PRIVACY_ID_COUNT 4u
+#define DPG_M_MEAN 8u
+#define DPG_M_VARIANCE 16u
+
+/* ---- partition selection (partition_selection.py:19-44) ---- */
+#define DPG_SELECT_NONE 0 /* public partitions: keep iff in public_mask */
+#define DPG_SELECT_TRUNCATED_GEOMETRIC 1
+#define DPG_SELECT_LAPLACE_THRESHOLD 2
+#define DPG_SELECT_GAUSSIAN_THRESHOLD 3
+
+/* ---- noise ---- */
+#define DPG_NOISE_NONE 0
+#define DPG_NOISE_LAPLACE 1
+#define DPG_NOISE_GAUSSIAN 2
+
+#define DPG_FAMILY_SCALAR 0   /* Count / Sum / PrivacyIdCount combiners    */
+#define DPG_FAMILY_MEAN 1     /* MeanCombiner (+ PrivacyIdCount)           */
+#define DPG_FAMILY_VARIANCE 2 /* VarianceCombiner (+ PrivacyIdCount)       */
+
+/* noise slots (each gets its own Philox counter) */
+#define DPG_SLOT_COUNT 0
+#define DPG_SLOT_SUM 1 /* SUM, or the normalised sum of MEAN/VARIANCE */
+#define DPG_SLOT_NSQ 2 /* normalised sum of squares (VARIANCE)        */
+#define DPG_SLOT_PID 3 /* PRIVACY_ID_COUNT                             */
+
+/* value-vector entries an output column can be mapped from */
+#define DPG_V_COUNT 0
+#define DPG_V_SUM 1
+#define DPG_V_MEAN 2
+#define DPG_V_VARIANCE 3
+#define DPG_V_PRIVACY_ID_COUNT 4
+
+typedef struct dpg_bound_params {
+    int32_t mode;        /* DPG_MODE_*                               */
+    int32_t sum_mode;    /* DPG_SUM_*                                */
+    uint32_t metric_mask;/* DPG_M_* accumulators to produce          */
+    int32_t reserved0;
+    int64_t max_partitions_contributed;      /* mpc (l0)            */
+    int64_t max_contributions_per_partition; /* mcpp (linf)         */
+    int64_t max_contributions;               /* L1 (PER_PRIVACY_ID) */
+    double min_value, max_value;
+    double min_sum_per_partition, max_sum_per_partition;
+    int64_t n_partitions;        /* P: pk ids are dense in [0, P)   */
+    const uint8_t *public_mask;  /* bitmap of P bits (device memory for
+                                    libdpg, host memory for the oracle);
+                                    NULL = private partition selection */
+} dpg_bound_params;
+
+/* Dense per-partition partial accumulators (structure of arrays).
+ * rows  = number of kept (privacy id, partition) pairs = privacy id count
+ * count = number of kept records; sum = bounded sum;
+ * nsum  = sum(clip(v) - mid), nsq = sum((clip(v) - mid)^2)
+ * Unused float arrays may be NULL. */
+typedef struct dpg_partials {
+    int64_t n_partitions;
+    int64_t *rows;
+    int64_t *count;
+    double *sum;
+    double *nsum;
+    double *nsq;
+} dpg_partials;
+
+typedef struct dpg_select_params {
+    int32_t strategy;            /* DPG_SELECT_*                          */
+    int32_t table_len;           /* truncated geometric: len(keep_table)  */
+    const double *keep_table;    /* host pointer; pi(n) for n < table_len,
+                                    1.0 beyond                              */
+    double threshold;            /* Laplace/Gaussian thresholding          */
+    double noise_scale;          /* b (Laplace) or sigma (Gaussian)        */
+    int64_t pre_threshold;       /* 0 = none                               */
+    int64_t max_rows_per_privacy_id; /* dp_engine.py:156-164 (normally 1)  */
+    int64_t pk_offset;           /* global pk id of partials index 0       */
+    const uint8_t *public_mask;  /* DPG_SELECT_NONE: keep iff bit set
+                                    (indexed by local partition id)        */
+} dpg_select_params;
+
+typedef struct dpg_noise_params {
+    int32_t noise_kind;  /* DPG_NOISE_*                                  */
+    int32_t family;      /* DPG_FAMILY_*                                 */
+    uint32_t slot_mask;  /* bit s: slot s exists (SCALAR / pid slot)     */
+    int32_t n_outputs;   /* output columns per partition                 */
+    int32_t out_src[8];  /* column j <- value vector entry DPG_V_*       */
+    double scale[4];     /* per-slot noise scale: b or sigma             */
+    double mid;          /* MEAN/VARIANCE range middle                   */
+    int32_t mean_const;  /* VARIANCE: min_value == max_value             */
+    int32_t msq_const;   /* VARIANCE: squares interval degenerate        */
+    double mean_const_value;
+    double msq_const_value;
+} dpg_noise_params;
+
+typedef struct dpg_ctx dpg_ctx;
+
+/* Context: device ordinal, 128-bit... (64-bit) seed of every keyed random
+ * stream. Returns NULL on failure. */
+dpg_ctx *dpg_ctx_create(int device, uint64_t seed);
+void dpg_ctx_destroy(dpg_ctx *ctx);
+int dpg_last_error(dpg_ctx *ctx, char *buf, size_t len);
+int dpg_set_seed(dpg_ctx *ctx, uint64_t seed);
+
+/* Contribution bounding + per-(pid,pk) accumulators + merge per partition.
+ * pid, pk: device int64[n]; value: device double[n] or NULL (COUNT / PID
+ * only).  out->* device arrays of out->n_partitions entries; they are
+ * zero-filled by the call.  stream: hipStream_t or NULL. */
+int dpg_bound_aggregate(dpg_ctx *ctx, const int64_t *pid, const int64_t *pk,
+                        const double *value, int64_t n,
+                        const dpg_bound_params *params, dpg_partials *out,
+                        void *stream);
+
+/* Partition selection + noise over dense partials (device arrays).
+ * keep: device uint8[P]; out: device double[P * noise->n_outputs]. */
+int dpg_select_and_noise(dpg_ctx *ctx, const dpg_partials *partials,
+                         const dpg_select_params *select,
+                         const dpg_noise_params *noise, uint8_t *keep,
+                         double *out, void *stream);
+
+/* Stream compaction of the kept partitions: writes the kept local ids to
+ * kept_ids (device int64[P]) and their output rows to kept_out (device
+ * double[P * n_outputs]); *n_kept (host) receives the count (synchronises
+ * the stream). */
+int dpg_compact_kept(dpg_ctx *ctx, const uint8_t *keep, const double *out,
+                     int64_t n_partitions, int32_t n_outputs,
+                     int64_t *kept_ids, double *kept_out, int64_t *n_kept,
+                     void *stream);
+
+/* Timing/profiling aid: per-stage device time (ms) of the last
+ * dpg_bound_aggregate call, measured with HIP events on its stream.
+ * names: "hist1","scatter1","hist2","scatter2","process","reduce", ... */
+int dpg_last_stage_times(dpg_ctx *ctx, char *names, size_t names_len,
+                         double *ms, int32_t max_stages, int32_t *n_stages);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DPG_H_ */

@@ -1,0 +1,427 @@
+/*
+ * dp_oracle.c -- CPU restatement of PipelineDP's DPEngine.aggregate hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load this library, and only as the
+ * checker / CPU baseline -- never as the thing measured or shipped.
+ *
+ * Parity pinning: the non-random part (grouping, clipping, accumulators,
+ * merge) is pinned by tests/golden/agg_*.npz, produced by running the
+ * reference itself (tests/golden/gen_golden.py).  The random part (which
+ * records / pairs survive sampling) follows the reference's *distribution*
+ * (uniform sampling without replacement) and is pinned by the chi-square
+ * fixture tests/golden/sampling_distribution.json.  The concrete sampler is
+ * the keyed-priority scheme of DESIGN.md section "Randomness", which the
+ * HIP kernels implement identically, so GPU-vs-oracle comparisons are exact
+ * even when bounding triggers.
+ *
+ * Reference call sites restated here (paths relative to /root/reference):
+ *   bounding:  pipeline_dp/contribution_bounders.py:56-105   (cross+per partition)
+ *              pipeline_dp/contribution_bounders.py:108-150  (per privacy id, L1)
+ *              pipeline_dp/contribution_bounders.py:153-195  (cross partition only)
+ *   sampling:  pipeline_dp/pipeline_backend.py:531-547, sampling_utils.py:19-29
+ *   combiners: pipeline_dp/combiners.py:255-256 (count), 296-297 (pid count),
+ *              348-353 (sum), 416-422 (mean), 491-500 (variance), 691-706
+ *   merge:     pipeline_dp/pipeline_backend.py:555-565
+ *   selection: pipeline_dp/dp_engine.py:305-361 ; PyDP partition_selection
+ *   noise:     pipeline_dp/dp_computations.py:120-184, 307-366, 541-576
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/dpg.h"
+
+/* ---------------------------------------------------------------- Philox */
+static inline void philox4x32_10(uint32_t c[4], const uint32_t k_in[2]) {
+    uint32_t k0 = k_in[0], k1 = k_in[1];
+    for (int r = 0; r < 10; ++r) {
+        uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+        uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+        uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        uint32_t n0 = hi1 ^ c[1] ^ k0;
+        uint32_t n1 = lo1;
+        uint32_t n2 = hi0 ^ c[3] ^ k1;
+        uint32_t n3 = lo0;
+        c[0] = n0; c[1] = n1; c[2] = n2; c[3] = n3;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+}
+
+void dpo_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+    uint32_t c[4] = {ctr[0], ctr[1], ctr[2], ctr[3]};
+    philox4x32_10(c, key);
+    memcpy(out, c, sizeof(c));
+}
+
+static inline uint32_t pair_prio(uint64_t seed, uint32_t pid, uint32_t pk) {
+    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32) ^ DPG_TAG_PAIR};
+    uint32_t c[4] = {pid, pk, 0u, 0u};
+    philox4x32_10(c, key);
+    return c[0];
+}
+
+static inline uint64_t rec_prio(uint64_t seed, uint32_t pid, uint32_t pk,
+                                uint64_t vbits, uint32_t occ) {
+    uint32_t key[2] = {(uint32_t)seed ^ (occ * 0x9E3779B9u),
+                       (uint32_t)(seed >> 32) ^ DPG_TAG_REC};
+    uint32_t c[4] = {pid, pk, (uint32_t)vbits, (uint32_t)(vbits >> 32)};
+    philox4x32_10(c, key);
+    return ((uint64_t)c[0] << 32) | c[1];
+}
+
+static inline double u53(uint32_t a, uint32_t b) {
+    uint64_t u = (((uint64_t)a << 32) | b) >> 11;
+    return ((double)u + 0.5) * 0x1.0p-53;
+}
+
+/* ----------------------------------------------------------- noise math */
+/* Granular ("snapped") Laplace / Gaussian, restating the secure samplers of
+ * the un-vendored Google DP library used by PyDP: the value
+ * is rounded to a power-of-two granularity g ~ scale * 2^-40 and the noise
+ * is an integer multiple of g. */
+double dpo_granularity(double scale) {
+    return exp2(ceil(log2(scale * 0x1.0p-40)));
+}
+
+double dpo_laplace(double x, double b, uint32_t u[4]) {
+    if (!(b > 0)) return x;
+    double g = dpo_granularity(b);
+    double e1 = -log(u53(u[0], u[1]));
+    double e2 = -log(u53(u[2], u[3]));
+    double k = floor(e1 * (b / g)) - floor(e2 * (b / g));
+    return rint(x / g) * g + k * g;
+}
+
+double dpo_gaussian(double x, double sigma, uint32_t u[4]) {
+    if (!(sigma > 0)) return x;
+    double g = dpo_granularity(sigma);
+    double r = sqrt(-2.0 * log(u53(u[0], u[1])));
+    double z = r * cos(6.283185307179586476925286766559 * u53(u[2], u[3]));
+    return rint(x / g) * g + rint(sigma * z / g) * g;
+}
+
+static void noise_uniforms(uint64_t seed, uint64_t pk, uint32_t slot,
+                           uint32_t out[4]) {
+    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32) ^ DPG_TAG_NOISE};
+    uint32_t c[4] = {(uint32_t)pk, (uint32_t)(pk >> 32), slot, 0u};
+    philox4x32_10(c, key);
+    memcpy(out, c, sizeof(c));
+}
+
+static void select_uniforms(uint64_t seed, uint64_t pk, uint32_t out[4]) {
+    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32) ^ DPG_TAG_SELECT};
+    uint32_t c[4] = {(uint32_t)pk, (uint32_t)(pk >> 32), 0u, 0u};
+    philox4x32_10(c, key);
+    memcpy(out, c, sizeof(c));
+}
+
+static double add_noise(int kind, double x, double scale, uint64_t seed,
+                        uint64_t pk, uint32_t slot) {
+    uint32_t u[4];
+    noise_uniforms(seed, pk, slot, u);
+    if (kind == DPG_NOISE_GAUSSIAN) return dpo_gaussian(x, scale, u);
+    if (kind == DPG_NOISE_LAPLACE) return dpo_laplace(x, scale, u);
+    return x; /* DPG_NOISE_NONE */
+}
+
+/* ------------------------------------------------------------- bounding */
+typedef struct {
+    const int64_t *pid, *pk;
+    const double *v;
+} cols_t;
+
+static const cols_t *g_cols;
+
+static inline uint64_t vbits_of(const double *v, int64_t i) {
+    uint64_t b = 0;
+    if (v) memcpy(&b, &v[i], 8);
+    return b;
+}
+
+/* order records by (pid, pk, value bits, index) */
+static int cmp_rec(const void *a, const void *b) {
+    int64_t i = *(const int64_t *)a, j = *(const int64_t *)b;
+    const cols_t *c = g_cols;
+    if (c->pid[i] != c->pid[j]) return c->pid[i] < c->pid[j] ? -1 : 1;
+    if (c->pk[i] != c->pk[j]) return c->pk[i] < c->pk[j] ? -1 : 1;
+    uint64_t vi = vbits_of(c->v, i), vj = vbits_of(c->v, j);
+    if (vi != vj) return vi < vj ? -1 : 1;
+    return i < j ? -1 : (i > j);
+}
+
+typedef struct {
+    uint64_t key;  /* selection key */
+    int64_t lo, hi; /* record range in the sorted index */
+} group_t;
+
+static int cmp_group(const void *a, const void *b) {
+    uint64_t x = ((const group_t *)a)->key, y = ((const group_t *)b)->key;
+    return x < y ? -1 : (x > y);
+}
+
+static inline double clip(double x, double lo, double hi) {
+    return x < lo ? lo : (x > hi ? hi : x);
+}
+
+/* accumulate one kept (pid, pk) pair whose kept records are idx[0..m) */
+static void emit_pair(const dpg_bound_params *p, const cols_t *c,
+                      const int64_t *idx, int64_t m, dpg_partials *out) {
+    if (m <= 0) return;
+    int64_t k = c->pk[idx[0]];
+    out->rows[k] += 1;
+    out->count[k] += m;
+    double mid = p->min_value + (p->max_value - p->min_value) / 2;
+    if (p->metric_mask & (DPG_M_SUM | DPG_M_MEAN | DPG_M_VARIANCE)) {
+        if (p->sum_mode == DPG_SUM_CLIP_PARTITION) {
+            double s = 0;
+            for (int64_t t = 0; t < m; ++t) s += c->v[idx[t]];
+            if (out->sum) out->sum[k] += clip(s, p->min_sum_per_partition,
+                                              p->max_sum_per_partition);
+        } else {
+            double s = 0, ns = 0, nq = 0;
+            for (int64_t t = 0; t < m; ++t) {
+                double x = clip(c->v[idx[t]], p->min_value, p->max_value);
+                s += x;
+                ns += x - mid;
+                nq += (x - mid) * (x - mid);
+            }
+            if (out->sum) out->sum[k] += s;
+            if (out->nsum) out->nsum[k] += ns;
+            if (out->nsq) out->nsq[k] += nq;
+        }
+    }
+}
+
+/* keep the `keep` records of sorted range [lo,hi) with the smallest record
+ * priority; ranges are sorted by (pid, pk, vbits) so identical records are
+ * adjacent and occ = position inside the run. Writes kept indices to dst. */
+static int64_t sample_records(uint64_t seed, const cols_t *c, const int64_t *ord,
+                              int64_t lo, int64_t hi, int64_t keep,
+                              int64_t *dst, uint64_t *tmpkey, int64_t *tmpidx) {
+    int64_t n = hi - lo;
+    if (n <= keep) {
+        memcpy(dst, ord + lo, n * sizeof(int64_t));
+        return n;
+    }
+    uint32_t occ = 0;
+    for (int64_t t = 0; t < n; ++t) {
+        int64_t i = ord[lo + t];
+        if (t > 0) {
+            int64_t j = ord[lo + t - 1];
+            occ = (c->pid[i] == c->pid[j] && c->pk[i] == c->pk[j] &&
+                   vbits_of(c->v, i) == vbits_of(c->v, j)) ? occ + 1 : 0;
+        }
+        tmpkey[t] = rec_prio(seed, (uint32_t)c->pid[i], (uint32_t)c->pk[i],
+                             vbits_of(c->v, i), occ);
+    }
+    /* selection of the `keep` smallest keys (ties: astronomically rare) */
+    for (int64_t t = 0; t < n; ++t) tmpidx[t] = t;
+    /* simple partial sort via full qsort on (key, t) pairs */
+    group_t *gs = (group_t *)malloc(n * sizeof(group_t));
+    for (int64_t t = 0; t < n; ++t) { gs[t].key = tmpkey[t]; gs[t].lo = t; }
+    qsort(gs, n, sizeof(group_t), cmp_group);
+    for (int64_t t = 0; t < keep; ++t) dst[t] = ord[lo + gs[t].lo];
+    free(gs);
+    return keep;
+}
+
+int dpo_bound_aggregate(uint64_t seed, const int64_t *pid, const int64_t *pk,
+                        const double *v, int64_t n, const dpg_bound_params *p,
+                        dpg_partials *out) {
+    cols_t c = {pid, pk, v};
+    for (int64_t i = 0; i < n; ++i) {
+        if (pid[i] < 0 || pid[i] > 0xFFFFFFFFll) return DPG_ERR_KEY_RANGE;
+        if (pk[i] < 0 || pk[i] >= p->n_partitions) return DPG_ERR_KEY_RANGE;
+    }
+    int64_t *ord = (int64_t *)malloc((n + 1) * sizeof(int64_t));
+    int64_t nn = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        if (p->public_mask &&
+            !((p->public_mask[pk[i] >> 3] >> (pk[i] & 7)) & 1))
+            continue; /* dp_engine.py:280-286 drop non-public partitions */
+        ord[nn++] = i;
+    }
+    g_cols = &c;
+    qsort(ord, nn, sizeof(int64_t), cmp_rec);
+    int64_t *kept = (int64_t *)malloc((nn + 1) * sizeof(int64_t));
+    int64_t *kept2 = (int64_t *)malloc((nn + 1) * sizeof(int64_t));
+    uint64_t *tkey = (uint64_t *)malloc((nn + 1) * sizeof(uint64_t));
+    int64_t *tidx = (int64_t *)malloc((nn + 1) * sizeof(int64_t));
+    group_t *pairs = (group_t *)malloc((nn + 1) * sizeof(group_t));
+
+    int64_t a = 0;
+    while (a < nn) {
+        int64_t b = a;
+        while (b < nn && pid[ord[b]] == pid[ord[a]]) ++b;
+        /* [a,b) = all records of one privacy id */
+        if (p->mode == DPG_MODE_PER_PRIVACY_ID) {
+            /* contribution_bounders.py:108-150: sample <= L records per pid,
+             * then group the kept ones by partition. ord[a,b) is sorted by
+             * (pk, vbits) so occ is the position inside identical runs. */
+            int64_t m = sample_records(seed, &c, ord, a, b,
+                                       p->max_contributions, kept, tkey, tidx);
+            /* regroup kept records by pk (kept is in priority order) */
+            qsort(kept, m, sizeof(int64_t), cmp_rec);
+            int64_t s = 0;
+            while (s < m) {
+                int64_t e = s;
+                while (e < m && pk[kept[e]] == pk[kept[s]]) ++e;
+                emit_pair(p, &c, kept + s, e - s, out);
+                s = e;
+            }
+        } else {
+            /* distinct pairs of this pid, with their selection keys */
+            int64_t np = 0, s = a;
+            while (s < b) {
+                int64_t e = s;
+                while (e < b && pk[ord[e]] == pk[ord[s]]) ++e;
+                uint32_t pp = pair_prio(seed, (uint32_t)pid[ord[s]],
+                                        (uint32_t)pk[ord[s]]);
+                pairs[np].key = ((uint64_t)pp << 32) | (uint32_t)pk[ord[s]];
+                pairs[np].lo = s;
+                pairs[np].hi = e;
+                ++np;
+                s = e;
+            }
+            int64_t keep_pairs = np;
+            if (np > p->max_partitions_contributed) {
+                /* contribution_bounders.py:90-92: uniform sample of mpc pairs */
+                qsort(pairs, np, sizeof(group_t), cmp_group);
+                keep_pairs = p->max_partitions_contributed;
+            }
+            for (int64_t q = 0; q < keep_pairs; ++q) {
+                int64_t lo = pairs[q].lo, hi = pairs[q].hi;
+                if (p->mode == DPG_MODE_CROSS_PARTITION) {
+                    /* contribution_bounders.py:153-195: all values */
+                    emit_pair(p, &c, ord + lo, hi - lo, out);
+                } else {
+                    /* contribution_bounders.py:74-76: <= mcpp per pair */
+                    int64_t m = sample_records(seed, &c, ord, lo, hi,
+                                               p->max_contributions_per_partition,
+                                               kept2, tkey, tidx);
+                    emit_pair(p, &c, kept2, m, out);
+                }
+            }
+        }
+        a = b;
+    }
+    free(ord); free(kept); free(kept2); free(tkey); free(tidx); free(pairs);
+    return DPG_OK;
+}
+
+/* ------------------------------------------------- selection + metrics */
+static int keep_partition(const dpg_select_params *s, uint64_t seed,
+                          uint64_t pk, int64_t local, int64_t rows) {
+    if (s->strategy == DPG_SELECT_NONE)  /* public partitions */
+        return s->public_mask ? ((s->public_mask[local >> 3] >> (local & 7)) & 1) : 1;
+    /* dp_engine.py:334-348: n = ceil(row_count / max_rows_per_privacy_id) */
+    if (rows <= 0) return 0;
+    int64_t n = (rows + s->max_rows_per_privacy_id - 1) / s->max_rows_per_privacy_id;
+    if (s->pre_threshold > 0) {
+        if (n < s->pre_threshold) return 0;
+        n = n - s->pre_threshold + 1;
+    }
+    uint32_t u[4];
+    select_uniforms(seed, pk, u);
+    switch (s->strategy) {
+    case DPG_SELECT_TRUNCATED_GEOMETRIC: {
+        double pr = n < s->table_len ? s->keep_table[n] : 1.0;
+        return u53(u[0], u[1]) < pr;
+    }
+    case DPG_SELECT_LAPLACE_THRESHOLD:
+        return dpo_laplace((double)n, s->noise_scale, u) > s->threshold;
+    case DPG_SELECT_GAUSSIAN_THRESHOLD:
+        return dpo_gaussian((double)n, s->noise_scale, u) > s->threshold;
+    }
+    return 0;
+}
+
+/* CompoundCombiner.compute_metrics for one partition: fills the value
+ * vector V[DPG_V_*] (combiners.py:262-263, 303-304, 358-359, 430-439,
+ * 508-520; dp_computations.py:307-366, 563-569). */
+void dpo_partition_metrics(const dpg_noise_params *z, uint64_t seed,
+                           uint64_t gk, double cnt, double sum, double nsum,
+                           double nsq, double pidc, double V[5]) {
+    int kind = z->noise_kind;
+    for (int j = 0; j < 5; ++j) V[j] = 0.0;
+    if (z->family == DPG_FAMILY_VARIANCE) {
+        double dcount = add_noise(kind, cnt, z->scale[DPG_SLOT_COUNT], seed, gk,
+                                  DPG_SLOT_COUNT);
+        double den = dcount > 1.0 ? dcount : 1.0;
+        double mean = z->mean_const
+                          ? z->mean_const_value
+                          : add_noise(kind, nsum, z->scale[DPG_SLOT_SUM], seed,
+                                      gk, DPG_SLOT_SUM) / den;
+        double msq = z->msq_const
+                         ? z->msq_const_value
+                         : add_noise(kind, nsq, z->scale[DPG_SLOT_NSQ], seed, gk,
+                                     DPG_SLOT_NSQ) / den;
+        double var = msq - mean * mean;
+        if (!z->mean_const) mean += z->mid;
+        V[DPG_V_VARIANCE] = var;
+        V[DPG_V_COUNT] = dcount;
+        V[DPG_V_SUM] = mean * dcount;
+        V[DPG_V_MEAN] = mean;
+    } else if (z->family == DPG_FAMILY_MEAN) {
+        double dcount = add_noise(kind, cnt, z->scale[DPG_SLOT_COUNT], seed, gk,
+                                  DPG_SLOT_COUNT);
+        double dn = add_noise(kind, nsum, z->scale[DPG_SLOT_SUM], seed, gk,
+                              DPG_SLOT_SUM);
+        double mean = z->mid + dn / (dcount > 1.0 ? dcount : 1.0);
+        V[DPG_V_COUNT] = dcount;
+        V[DPG_V_SUM] = mean * dcount;
+        V[DPG_V_MEAN] = mean;
+    } else {
+        if (z->slot_mask & (1u << DPG_SLOT_COUNT))
+            V[DPG_V_COUNT] = add_noise(kind, cnt, z->scale[DPG_SLOT_COUNT], seed,
+                                       gk, DPG_SLOT_COUNT);
+        if (z->slot_mask & (1u << DPG_SLOT_SUM))
+            V[DPG_V_SUM] = add_noise(kind, sum, z->scale[DPG_SLOT_SUM], seed, gk,
+                                     DPG_SLOT_SUM);
+    }
+    if (z->slot_mask & (1u << DPG_SLOT_PID))
+        V[DPG_V_PRIVACY_ID_COUNT] = add_noise(kind, pidc, z->scale[DPG_SLOT_PID],
+                                              seed, gk, DPG_SLOT_PID);
+}
+
+int dpo_select_and_noise(uint64_t seed, const dpg_partials *in,
+                         const dpg_select_params *s, const dpg_noise_params *z,
+                         uint8_t *keep, double *out) {
+    int64_t P = in->n_partitions;
+    for (int64_t k = 0; k < P; ++k) {
+        uint64_t gk = (uint64_t)(k + s->pk_offset);
+        int kp = keep_partition(s, seed, gk, k, in->rows[k]);
+        keep[k] = (uint8_t)kp;
+        double *o = out + k * z->n_outputs;
+        for (int j = 0; j < z->n_outputs; ++j) o[j] = 0.0;
+        if (!kp) continue;
+        double V[5];
+        dpo_partition_metrics(z, seed, gk, (double)in->count[k],
+                              in->sum ? in->sum[k] : 0.0,
+                              in->nsum ? in->nsum[k] : 0.0,
+                              in->nsq ? in->nsq[k] : 0.0, (double)in->rows[k], V);
+        for (int j = 0; j < z->n_outputs; ++j) o[j] = V[z->out_src[j]];
+    }
+    return DPG_OK;
+}
+
+/* exported helpers for distribution tests */
+uint32_t dpo_pair_prio(uint64_t seed, uint32_t pid, uint32_t pk) {
+    return pair_prio(seed, pid, pk);
+}
+uint64_t dpo_rec_prio(uint64_t seed, uint32_t pid, uint32_t pk, uint64_t vbits,
+                      uint32_t occ) {
+    return rec_prio(seed, pid, pk, vbits, occ);
+}
+double dpo_noise_sample(int kind, double x, double scale, uint64_t seed,
+                        uint64_t pk, uint32_t slot) {
+    return add_noise(kind, x, scale, seed, pk, slot);
+}
+int dpo_keep_partition(const dpg_select_params *s, uint64_t seed, uint64_t pk,
+                       int64_t rows) {
+    return keep_partition(s, seed, pk, 0, rows);
+}

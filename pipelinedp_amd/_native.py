@@ -1,0 +1,183 @@
+"""ctypes binding of libdpg.so (include/dpg.h).
+
+The library is built in-tree by __graft_entry__.build() into
+pipelinedp_amd/lib/libdpg.so.  There is no CPU fallback: if the library or a
+GPU is missing, every device entry point raises.
+"""
+import ctypes
+import os
+import threading
+
+_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libdpg.so")
+
+DPG_OK = 0
+ERRORS = {1: "invalid argument", 2: "key out of range", 3: "HIP error",
+          4: "out of device memory", 5: "unsupported"}
+
+EXPORTED = ("dpg_ctx_create", "dpg_ctx_destroy", "dpg_last_error", "dpg_set_seed",
+            "dpg_bound_aggregate", "dpg_select_and_noise", "dpg_compact_kept",
+            "dpg_last_stage_times")
+
+
+class BoundParams(ctypes.Structure):
+    _fields_ = [("mode", ctypes.c_int32), ("sum_mode", ctypes.c_int32),
+                ("metric_mask", ctypes.c_uint32), ("reserved0", ctypes.c_int32),
+                ("max_partitions_contributed", ctypes.c_int64),
+                ("max_contributions_per_partition", ctypes.c_int64),
+                ("max_contributions", ctypes.c_int64),
+                ("min_value", ctypes.c_double), ("max_value", ctypes.c_double),
+                ("min_sum_per_partition", ctypes.c_double),
+                ("max_sum_per_partition", ctypes.c_double),
+                ("n_partitions", ctypes.c_int64), ("public_mask", ctypes.c_void_p)]
+
+
+class Partials(ctypes.Structure):
+    _fields_ = [("n_partitions", ctypes.c_int64), ("rows", ctypes.c_void_p),
+                ("count", ctypes.c_void_p), ("sum", ctypes.c_void_p),
+                ("nsum", ctypes.c_void_p), ("nsq", ctypes.c_void_p)]
+
+
+class SelectParams(ctypes.Structure):
+    _fields_ = [("strategy", ctypes.c_int32), ("table_len", ctypes.c_int32),
+                ("keep_table", ctypes.c_void_p), ("threshold", ctypes.c_double),
+                ("noise_scale", ctypes.c_double), ("pre_threshold", ctypes.c_int64),
+                ("max_rows_per_privacy_id", ctypes.c_int64),
+                ("pk_offset", ctypes.c_int64), ("public_mask", ctypes.c_void_p)]
+
+
+class NoiseParams(ctypes.Structure):
+    _fields_ = [("noise_kind", ctypes.c_int32), ("family", ctypes.c_int32),
+                ("slot_mask", ctypes.c_uint32), ("n_outputs", ctypes.c_int32),
+                ("out_src", ctypes.c_int32 * 8), ("scale", ctypes.c_double * 4),
+                ("mid", ctypes.c_double), ("mean_const", ctypes.c_int32),
+                ("msq_const", ctypes.c_int32), ("mean_const_value", ctypes.c_double),
+                ("msq_const_value", ctypes.c_double)]
+
+
+def fill(struct_type, fields: dict):
+    s = struct_type()
+    for k, v in fields.items():
+        if k in ("out_src", "scale"):
+            arr = getattr(s, k)
+            for i, x in enumerate(v):
+                arr[i] = x
+        else:
+            setattr(s, k, v)
+    return s
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def library_path() -> str:
+    return _LIB_PATH
+
+
+def load():
+    """Loads libdpg.so; raises NativeError if it was not built."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(_LIB_PATH):
+            raise NativeError(
+                f"{_LIB_PATH} is missing: build it with "
+                f"`python -c 'import __graft_entry__ as g; g.build()'`. "
+                f"There is no CPU fallback for the MI355X hot path.")
+        lib = ctypes.CDLL(_LIB_PATH)
+        vp, i64, i32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32
+        lib.dpg_ctx_create.argtypes = [ctypes.c_int, ctypes.c_uint64]
+        lib.dpg_ctx_create.restype = vp
+        lib.dpg_ctx_destroy.argtypes = [vp]
+        lib.dpg_ctx_destroy.restype = None
+        lib.dpg_last_error.argtypes = [vp, ctypes.c_char_p, ctypes.c_size_t]
+        lib.dpg_last_error.restype = ctypes.c_int
+        lib.dpg_set_seed.argtypes = [vp, ctypes.c_uint64]
+        lib.dpg_set_seed.restype = ctypes.c_int
+        lib.dpg_bound_aggregate.argtypes = [vp, vp, vp, vp, i64,
+                                            ctypes.POINTER(BoundParams),
+                                            ctypes.POINTER(Partials), vp]
+        lib.dpg_bound_aggregate.restype = ctypes.c_int
+        lib.dpg_select_and_noise.argtypes = [vp, ctypes.POINTER(Partials),
+                                             ctypes.POINTER(SelectParams),
+                                             ctypes.POINTER(NoiseParams), vp, vp, vp]
+        lib.dpg_select_and_noise.restype = ctypes.c_int
+        lib.dpg_compact_kept.argtypes = [vp, vp, vp, i64, i32, vp, vp,
+                                         ctypes.POINTER(ctypes.c_int64), vp]
+        lib.dpg_compact_kept.restype = ctypes.c_int
+        lib.dpg_last_stage_times.argtypes = [vp, ctypes.c_char_p, ctypes.c_size_t,
+                                             ctypes.POINTER(ctypes.c_double), i32,
+                                             ctypes.POINTER(ctypes.c_int32)]
+        lib.dpg_last_stage_times.restype = ctypes.c_int
+        _lib = lib
+        return lib
+
+
+class Context:
+    """Owns one dpg_ctx (one device, one seed)."""
+
+    def __init__(self, device: int, seed: int):
+        self.lib = load()
+        self.device = device
+        self.handle = self.lib.dpg_ctx_create(int(device), ctypes.c_uint64(seed & (2**64 - 1)))
+        if not self.handle:
+            raise NativeError(f"dpg_ctx_create failed on device {device}")
+
+    def close(self):
+        if self.handle:
+            self.lib.dpg_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def check(self, status: int, what: str):
+        if status == DPG_OK:
+            return
+        buf = ctypes.create_string_buffer(1024)
+        self.lib.dpg_last_error(self.handle, buf, 1024)
+        msg = buf.value.decode(errors="replace")
+        if status == 2:
+            raise ValueError(f"{what}: {msg}")
+        raise NativeError(f"{what} failed ({ERRORS.get(status, status)}): {msg}")
+
+    def set_seed(self, seed: int):
+        self.check(self.lib.dpg_set_seed(self.handle, ctypes.c_uint64(seed & (2**64 - 1))),
+                   "dpg_set_seed")
+
+    def bound_aggregate(self, pid_ptr, pk_ptr, value_ptr, n, bound: BoundParams,
+                        partials: Partials, stream):
+        st = self.lib.dpg_bound_aggregate(self.handle, pid_ptr, pk_ptr, value_ptr, n,
+                                          ctypes.byref(bound), ctypes.byref(partials), stream)
+        self.check(st, "dpg_bound_aggregate")
+
+    def select_and_noise(self, partials: Partials, sel: SelectParams, noise: NoiseParams,
+                         keep_ptr, out_ptr, stream):
+        st = self.lib.dpg_select_and_noise(self.handle, ctypes.byref(partials),
+                                           ctypes.byref(sel), ctypes.byref(noise),
+                                           keep_ptr, out_ptr, stream)
+        self.check(st, "dpg_select_and_noise")
+
+    def compact(self, keep_ptr, out_ptr, n_partitions, n_out, ids_ptr, kept_out_ptr, stream) -> int:
+        n = ctypes.c_int64(0)
+        st = self.lib.dpg_compact_kept(self.handle, keep_ptr, out_ptr, n_partitions, n_out,
+                                       ids_ptr, kept_out_ptr, ctypes.byref(n), stream)
+        self.check(st, "dpg_compact_kept")
+        return n.value
+
+    def stage_times(self):
+        names = ctypes.create_string_buffer(1024)
+        ms = (ctypes.c_double * 32)()
+        ns = ctypes.c_int32(0)
+        self.check(self.lib.dpg_last_stage_times(self.handle, names, 1024, ms, 32,
+                                                 ctypes.byref(ns)), "stage_times")
+        keys = names.value.decode().split(",") if ns.value else []
+        return dict(zip(keys, [ms[i] for i in range(ns.value)]))

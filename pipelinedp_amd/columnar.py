@@ -1,0 +1,213 @@
+"""Ingest: turn the user's collection into device columns for the kernels.
+
+The reference extracts `(privacy_id, partition_key, value)` per row with the
+DataExtractors callables (dp_engine.py:384-397).  The MI355X path keeps the
+same extractors but prefers columnar input:
+
+* `ColumnarData` / a mapping of columns (numpy arrays or torch tensors,
+  ideally already on the GPU).  An extractor is then a column name or a
+  callable applied to the whole container.
+* Any other iterable is treated as rows; the extractors run per row on the
+  host (reference behaviour, slow, meant for small inputs).
+
+Keys: the kernels need privacy ids in [0, 2^32-1) and dense partition ids
+in [0, P).  Integer keys that already satisfy this are used as they are;
+anything else (strings, tuples, huge or negative ints) is dictionary-encoded
+(`unique` + inverse), and the partition dictionary maps results back.
+Encoding is ingest, not part of the DP computation.
+"""
+import dataclasses
+from collections.abc import Mapping
+from typing import Any, Optional, Sequence
+
+import numpy as np
+import torch
+
+_PID_LIMIT = 0xFFFFFFFF  # exclusive
+
+
+@dataclasses.dataclass
+class ColumnarData:
+    """Columnar collection for DPEngine.aggregate on the MI355X backend.
+
+    `n_partitions`: if given, `pk` must already hold dense ids in
+    [0, n_partitions) and is passed to the device unchecked (the kernel still
+    rejects out-of-range keys with ValueError)."""
+    pid: Any = None
+    pk: Any = None
+    value: Any = None
+    n_partitions: Optional[int] = None
+
+    def __getitem__(self, name):
+        return getattr(self, name)
+
+    def __len__(self):
+        return len(self.pk)
+
+    def __bool__(self):
+        return self.pk is not None and len(self.pk) > 0
+
+
+@dataclasses.dataclass
+class EncodedInput:
+    pid: Optional[torch.Tensor]
+    pk: torch.Tensor
+    value: Optional[torch.Tensor]
+    n: int
+    n_partitions: int
+    key_table: Optional[Sequence]  # dense id -> original key (None: identity)
+    public_mask: Optional[torch.Tensor] = None  # uint8 bitmap on the device
+    public_count: int = 0
+
+
+def _extract(col, extractor):
+    if extractor is None:
+        return None
+    if isinstance(extractor, str):
+        return col[extractor]
+    return extractor(col)
+
+
+def _is_columnar(col) -> bool:
+    return isinstance(col, (ColumnarData, Mapping))
+
+
+def _to_tensor(x, device) -> torch.Tensor:
+    if isinstance(x, torch.Tensor):
+        return x.to(device) if x.device != device else x
+    a = np.asarray(x)
+    return torch.from_numpy(np.ascontiguousarray(a)).to(device)
+
+
+def _integer_like(x) -> bool:
+    if isinstance(x, torch.Tensor):
+        return not x.is_floating_point() and not x.is_complex() and x.dtype != torch.bool
+    return np.asarray(x).dtype.kind in "iu"
+
+
+def _encode_keys(values, device, extra=None):
+    """Dictionary-encodes arbitrary keys; returns (ids tensor, key table,
+    ids of `extra`)."""
+    if isinstance(values, torch.Tensor) and _integer_like(values):
+        both = values if extra is None else torch.cat(
+            [values, torch.as_tensor(np.asarray(list(extra), dtype=np.int64), device=values.device)])
+        uniq, inv = torch.unique(both, return_inverse=True)
+        n = values.numel()
+        return (inv[:n].to(torch.int64).to(device), uniq.cpu().numpy(),
+                None if extra is None else inv[n:].cpu().numpy())
+    arr = np.asarray(values, dtype=object) if not isinstance(values, np.ndarray) else values
+    if extra is not None:
+        arr = np.concatenate([np.asarray(arr, dtype=object),
+                              np.asarray(list(extra), dtype=object)])
+    try:
+        uniq, inv = np.unique(arr, return_inverse=True)
+        table = list(uniq)
+    except TypeError:  # unorderable keys: first-seen order
+        index = {}
+        inv = np.empty(len(arr), dtype=np.int64)
+        for i, k in enumerate(arr.tolist()):
+            inv[i] = index.setdefault(k, len(index))
+        table = list(index)
+    n = len(values)
+    ids = torch.from_numpy(np.ascontiguousarray(inv[:n].astype(np.int64))).to(device)
+    return ids, table, (None if extra is None else inv[n:])
+
+
+def _range(t: torch.Tensor):
+    if t.numel() == 0:
+        return 0, -1
+    return int(t.min().item()), int(t.max().item())
+
+
+def encode(col, extractors, device: torch.device, need_values: bool,
+           public_partitions=None, need_pid: bool = True) -> EncodedInput:
+    if _is_columnar(col):
+        pid = _extract(col, extractors.privacy_id_extractor) if need_pid else None
+        pk = _extract(col, extractors.partition_extractor)
+        value = _extract(col, extractors.value_extractor) if need_values else None
+        hint = col.n_partitions if isinstance(col, ColumnarData) else col.get("n_partitions")
+    else:
+        rows = col if isinstance(col, list) else list(col)
+        ex = extractors
+        pid = [ex.privacy_id_extractor(r) for r in rows] if need_pid else None
+        pk = [ex.partition_extractor(r) for r in rows]
+        value = ([ex.value_extractor(r) for r in rows]
+                 if need_values and ex.value_extractor is not None else None)
+        hint = None
+    if pk is None:
+        raise ValueError("partition_extractor must be set")
+    n = len(pk)
+    if need_values and value is None:
+        raise ValueError("value_extractor must be set for SUM, MEAN and VARIANCE")
+
+    # ---- partition keys -> dense ids
+    public_list = None if public_partitions is None else list(public_partitions)
+    key_table = None
+    pk_ids = None
+    public_ids = None
+    if _integer_like(pk):
+        pk_t = _to_tensor(pk, device).to(torch.int64)
+        if hint is not None:
+            P = int(hint)
+            pk_ids = pk_t
+            if public_list is not None:
+                public_ids = np.asarray(public_list, dtype=np.int64)
+        else:
+            lo, hi = _range(pk_t)
+            pub_arr = None
+            if public_list is not None:
+                try:
+                    pub_arr = np.asarray(public_list, dtype=np.int64)
+                except (TypeError, ValueError, OverflowError):
+                    pub_arr = None
+                if pub_arr is not None and pub_arr.size:
+                    lo, hi = min(lo, int(pub_arr.min())), max(hi, int(pub_arr.max()))
+            dense_ok = lo >= 0 and hi + 1 <= max(1 << 20, 4 * max(n, 1)) and (
+                public_list is None or pub_arr is not None)
+            if dense_ok:
+                pk_ids, P = pk_t, max(hi + 1, 1)
+                public_ids = pub_arr
+            else:
+                pk_ids, key_table, public_ids = _encode_keys(pk_t, device, public_list)
+                P = max(len(key_table), 1)
+    else:
+        pk_ids, key_table, public_ids = _encode_keys(pk, device, public_list)
+        P = max(len(key_table), 1)
+
+    # ---- privacy ids -> [0, 2^32-1)
+    pid_ids = None
+    if need_pid:
+        if pid is None:
+            raise ValueError("privacy_id_extractor must be set")
+        if _integer_like(pid):
+            pid_t = _to_tensor(pid, device).to(torch.int64)
+            if hint is None:
+                lo, hi = _range(pid_t)
+                if lo < 0 or hi >= _PID_LIMIT:
+                    pid_t, _, _ = _encode_keys(pid_t, device)
+            pid_ids = pid_t
+        else:
+            pid_ids, _, _ = _encode_keys(pid, device)
+
+    val = None
+    if need_values:
+        val = _to_tensor(value, device).to(torch.float64)
+
+    enc = EncodedInput(pid=pid_ids, pk=pk_ids.contiguous(), value=val, n=n,
+                       n_partitions=int(P), key_table=key_table)
+    if public_ids is not None:
+        mask = np.zeros((P + 7) // 8, dtype=np.uint8)
+        ids = np.unique(np.asarray(public_ids, dtype=np.int64))
+        ids = ids[(ids >= 0) & (ids < P)]
+        np.bitwise_or.at(mask, ids >> 3, (1 << (ids & 7)).astype(np.uint8))
+        enc.public_mask = torch.from_numpy(mask).to(device)
+        enc.public_count = int(ids.size)
+    if enc.pid is not None:
+        enc.pid = enc.pid.contiguous()
+    return enc
+
+
+def decode_keys(ids: np.ndarray, key_table) -> list:
+    if key_table is None:
+        return ids.tolist()
+    return [key_table[i] for i in ids.tolist()]

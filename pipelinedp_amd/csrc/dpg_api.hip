@@ -1,0 +1,481 @@
+// dpg_api.hip -- C ABI + host orchestration of the MI355X DPEngine.aggregate
+// hot path.  Build: hipcc --offload-arch=gfx950 -O3 -shared -fPIC.
+//
+// Pipeline of dpg_bound_aggregate (DESIGN.md "Kernels"):
+//   partition levels (hist, scan, digit base, scatter) by privacy-id hash
+//   -> k_bound_lds (+ k_bound_global for oversize buckets)
+//   -> one partition-key-range level over the kept pairs -> k_reduce_items
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "dpg_bound.h"
+#include "dpg_common.h"
+#include "dpg_partition.h"
+#include "dpg_select.h"
+
+using namespace dpg;
+
+namespace {
+
+constexpr uint32_t kBucketCap = 2048;      // records per bucket processed in LDS
+constexpr uint32_t kBucketTarget = 1024;   // average bucket size the levels aim for
+constexpr int kMaxLevels = 3;
+
+struct Buf {
+    void *p = nullptr;
+    size_t bytes = 0;
+};
+
+struct Control {  // device-side counters, zeroed per call
+    uint32_t err;
+    uint32_t queue;
+    uint32_t item_cursor;
+    uint32_t n_oversize;
+    uint32_t ntiles[8];
+    int64_t nvalid;
+    int64_t n_scalar;
+    int64_t kept_total;
+    uint32_t pad[4];
+};
+
+}  // namespace
+
+struct dpg_ctx {
+    int device = 0;
+    uint64_t seed = 0;
+    int n_cu = 256;
+    std::string err;
+    std::map<std::string, Buf> bufs;
+    std::vector<std::string> stage_names;
+    std::vector<hipEvent_t> events;
+    int n_events_used = 0;
+    hipStream_t last_stream = nullptr;
+};
+
+namespace {
+
+int fail(dpg_ctx *c, int code, const std::string &msg) {
+    if (c) c->err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                     \
+    do {                                                                                  \
+        hipError_t e_ = (expr);                                                           \
+        if (e_ != hipSuccess)                                                             \
+            return fail(ctx, DPG_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+#define LAUNCH_CHECK()                                                                        \
+    do {                                                                                      \
+        hipError_t e_ = hipGetLastError();                                                    \
+        if (e_ != hipSuccess)                                                                 \
+            return fail(ctx, DPG_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(e_)); \
+    } while (0)
+
+void *ws(dpg_ctx *ctx, const char *name, size_t bytes, int *status) {
+    Buf &b = ctx->bufs[name];
+    if (b.bytes >= bytes && b.p) return b.p;
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+    size_t want = std::max<size_t>(bytes, 256);
+    if (hipMalloc(&b.p, want) != hipSuccess) {
+        (void)hipGetLastError();
+        *status = fail(ctx, DPG_ERR_OOM, std::string("out of device memory allocating ") + name +
+                                             " (" + std::to_string(want) + " bytes)");
+        return nullptr;
+    }
+    b.bytes = want;
+    return b.p;
+}
+
+#define WS(ptr, T, name, count)                                           \
+    T *ptr = reinterpret_cast<T *>(ws(ctx, name, sizeof(T) * (size_t)(count), &st)); \
+    if (!ptr) return st;
+
+void stage(dpg_ctx *ctx, hipStream_t s, const char *name) {
+    if (ctx->n_events_used >= (int)ctx->events.size()) {
+        hipEvent_t e;
+        (void)hipEventCreate(&e);
+        ctx->events.push_back(e);
+    }
+    (void)hipEventRecord(ctx->events[ctx->n_events_used++], s);
+    ctx->stage_names.push_back(name);
+}
+
+uint32_t ceil_log2(double x) {
+    if (x <= 1.0) return 0;
+    return (uint32_t)std::ceil(std::log2(x));
+}
+
+// One partition level over `S` segments of `in` (or the SoA input).
+template <class Src, class Rec, class Dig, int IPT>
+int run_level(dpg_ctx *ctx, hipStream_t s, Src src, Dig dig, uint32_t S, const int64_t *seg_start,
+              const uint32_t *seg_cnt, const int64_t *seg_cnt64, int64_t n_upper, uint32_t F,
+              uint32_t bits, Rec *out, const char *tag, int64_t **base_out, uint32_t **tot_out,
+              uint32_t *ntiles_dev) {
+    int st = DPG_OK;
+    const int64_t sub = (int64_t)kPartThreads * IPT;
+    int64_t tile = std::max<int64_t>(sub, ((n_upper / 3072 + sub - 1) / sub) * sub);
+    uint32_t max_tiles = (uint32_t)(n_upper / tile + S + 1);
+    std::string t(tag);
+    WS(tiles, TileDesc, (t + ".tiles").c_str(), max_tiles);
+    WS(stb, uint32_t, (t + ".stb").c_str(), S);
+    WS(snt, uint32_t, (t + ".snt").c_str(), S);
+    WS(hist, uint32_t, (t + ".hist").c_str(), (size_t)max_tiles * F);
+    WS(tot, uint32_t, (t + ".tot").c_str(), (size_t)S * F);
+    WS(base, int64_t, (t + ".base").c_str(), (size_t)S * F);
+    k_build_tiles<<<(S + 255) / 256, 256, 0, s>>>(seg_start, seg_cnt, seg_cnt64, S, tile, tiles, stb,
+                                                  snt, ntiles_dev);
+    LAUNCH_CHECK();
+    k_hist<Src, Rec, Dig><<<max_tiles, kPartThreads, 4 * F * sizeof(uint32_t), s>>>(
+        src, dig, tiles, ntiles_dev, F, hist);
+    LAUNCH_CHECK();
+    k_scan_tiles<<<dim3(S, (F + 63) / 64), 1024, 0, s>>>(stb, snt, F, hist, tot);
+    LAUNCH_CHECK();
+    k_digit_base<<<S, 1024, 0, s>>>(seg_start, F, tot, base, nullptr);
+    LAUNCH_CHECK();
+    size_t lds = sizeof(Rec) * sub + 1024 * 4 * 2 + 1024 * 8 + 16 * 4;
+    k_scatter<Src, Rec, Dig, IPT><<<max_tiles, kPartThreads, lds, s>>>(src, dig, tiles, ntiles_dev,
+                                                                      F, bits, hist, base, out);
+    LAUNCH_CHECK();
+    *base_out = base;
+    *tot_out = tot;
+    return DPG_OK;
+}
+
+BoundParams to_bound(const dpg_bound_params *p, uint64_t seed) {
+    BoundParams b;
+    b.mode = p->mode;
+    b.sum_mode = p->sum_mode;
+    b.mask = p->metric_mask;
+    b.need_values = (p->metric_mask & (DPG_M_SUM | DPG_M_MEAN | DPG_M_VARIANCE)) != 0;
+    b.mpc = (uint32_t)std::min<int64_t>(p->max_partitions_contributed, 0x7FFFFFFF);
+    b.mcpp = (uint32_t)std::min<int64_t>(p->max_contributions_per_partition, 0x7FFFFFFF);
+    b.L = (uint32_t)std::min<int64_t>(p->max_contributions, 0x7FFFFFFF);
+    b.lo = p->min_value;
+    b.hi = p->max_value;
+    b.lo_pp = p->min_sum_per_partition;
+    b.hi_pp = p->max_sum_per_partition;
+    b.mid = p->min_value + (p->max_value - p->min_value) / 2;
+    b.seed = seed;
+    return b;
+}
+
+template <class Item>
+int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Rec16 *recs, const int64_t *bstart,
+                     const uint32_t *bcnt, uint32_t B, const BoundParams &bp, Item *items,
+                     Item *items2, int64_t n, int64_t P, const dpg_partials *out, Control *ctl) {
+    int st = DPG_OK;
+    WS(oversize, uint32_t, "bound.oversize", B);
+    const size_t lds = BucketLayout::make(kBucketCap, ItemTraits<Item>::var, 2).total +
+                       align16(sizeof(BucketShared));
+    stage(ctx, s, "bound");
+    k_bound_lds<Item><<<ctx->n_cu, kBoundThreads, lds, s>>>(
+        recs, bstart, bcnt, B, kBucketCap, &ctl->queue, bp, items, &ctl->item_cursor, oversize,
+        &ctl->n_oversize);
+    LAUNCH_CHECK();
+    // oversize buckets (rare): global-memory working sets
+    Control hctl;
+    HIP_TRY(hipMemcpyAsync(&hctl, ctl, sizeof(Control), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (hctl.err) return fail(ctx, DPG_ERR_KEY_RANGE,
+                              "privacy id outside [0, 2^32-1) or partition key outside [0, P)");
+    if (hctl.n_oversize > 0) {
+        const uint32_t no = hctl.n_oversize;
+        std::vector<uint32_t> list(no), cnt(B);
+        HIP_TRY(hipMemcpy(list.data(), oversize, no * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(cnt.data(), bcnt, (size_t)B * 4, hipMemcpyDeviceToHost));
+        std::vector<size_t> off(no);
+        size_t total = 0;
+        for (uint32_t i = 0; i < no; ++i) {
+            off[i] = total;
+            total += align16(BucketLayout::make(cnt[list[i]], ItemTraits<Item>::var, 4).total);
+        }
+        WS(scratch, char, "bound.scratch", total);
+        WS(doff, size_t, "bound.scratch_off", no);
+        HIP_TRY(hipMemcpyAsync(doff, off.data(), no * sizeof(size_t), hipMemcpyHostToDevice, s));
+        k_bound_global<Item><<<no, kBoundThreads, 0, s>>>(recs, bstart, bcnt, oversize, doff,
+                                                          scratch, bp, items, &ctl->item_cursor);
+        LAUNCH_CHECK();
+    }
+    // ---- merge kept pairs per partition
+    stage(ctx, s, "reduce");
+    Partials po{out->rows, out->count, out->sum, out->nsum, out->nsq};
+    const int64_t nranges = (P + kRange - 1) / kRange;
+    if (nranges <= 1024) {
+        uint32_t F = (uint32_t)std::max<int64_t>(1, nranges);
+        uint32_t bits = std::max<uint32_t>(1, ceil_log2((double)F));
+        int64_t *baseR;
+        uint32_t *totR;
+        int r = run_level<SrcAoS<Item>, Item, DigPk<Item>, (sizeof(Item) == 16 ? 8 : 4)>(
+            ctx, s, SrcAoS<Item>{items}, DigPk<Item>{(uint32_t)kRangeBits}, 1u, nullptr,
+            &ctl->item_cursor, nullptr, n, F, bits, items2, "items", &baseR, &totR,
+            &ctl->ntiles[4]);
+        if (r) return r;
+        const int64_t rtile = 65536;
+        uint32_t max_tiles = (uint32_t)(n / rtile + F + 1);
+        WS(rt, TileDesc, "reduce.tiles", max_tiles);
+        WS(rstb, uint32_t, "reduce.stb", F);
+        WS(rsnt, uint32_t, "reduce.snt", F);
+        k_build_tiles<<<(F + 255) / 256, 256, 0, s>>>(baseR, totR, nullptr, F, rtile, rt, rstb,
+                                                      rsnt, &ctl->ntiles[5]);
+        LAUNCH_CHECK();
+        size_t lds_r = (size_t)kRange * (ItemTraits<Item>::var ? 3 * 8 : 8) + kRange * 8;
+        k_reduce_items<Item><<<max_tiles, 1024, lds_r, s>>>(items2, rt, &ctl->ntiles[5], P, po);
+        LAUNCH_CHECK();
+    } else {
+        k_reduce_items_direct<Item><<<ctx->n_cu * 8, 256, 0, s>>>(items, &ctl->item_cursor, po);
+        LAUNCH_CHECK();
+    }
+    stage(ctx, s, "end");
+    return DPG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+dpg_ctx *dpg_ctx_create(int device, uint64_t seed) {
+    if (hipSetDevice(device) != hipSuccess) return nullptr;
+    dpg_ctx *c = new dpg_ctx();
+    c->device = device;
+    c->seed = seed;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->n_cu = prop.multiProcessorCount;
+    // the bound kernel needs ~150 KB of dynamic LDS
+    (void)hipFuncSetAttribute((const void *)k_bound_lds<Item16>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void *)k_bound_lds<Item32>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    return c;
+}
+
+void dpg_ctx_destroy(dpg_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    for (auto &kv : c->bufs)
+        if (kv.second.p) (void)hipFree(kv.second.p);
+    for (auto e : c->events) (void)hipEventDestroy(e);
+    delete c;
+}
+
+int dpg_last_error(dpg_ctx *c, char *buf, size_t len) {
+    if (!c || !buf || len == 0) return DPG_ERR_INVALID_ARG;
+    std::snprintf(buf, len, "%s", c->err.c_str());
+    return DPG_OK;
+}
+
+int dpg_set_seed(dpg_ctx *c, uint64_t seed) {
+    if (!c) return DPG_ERR_INVALID_ARG;
+    c->seed = seed;
+    return DPG_OK;
+}
+
+int dpg_bound_aggregate(dpg_ctx *ctx, const int64_t *pid, const int64_t *pk, const double *value,
+                        int64_t n, const dpg_bound_params *p, dpg_partials *out, void *stream) {
+    if (!ctx) return DPG_ERR_INVALID_ARG;
+    if (!p || !out || n < 0 || (n > 0 && (!pid || !pk)))
+        return fail(ctx, DPG_ERR_INVALID_ARG, "null argument");
+    if (p->n_partitions <= 0 || p->n_partitions >= 0xFFFFFFFFll)
+        return fail(ctx, DPG_ERR_INVALID_ARG, "n_partitions must be in [1, 2^32-1)");
+    if (out->n_partitions != p->n_partitions || !out->rows || !out->count)
+        return fail(ctx, DPG_ERR_INVALID_ARG, "partials must cover n_partitions");
+    if (p->mode < 0 || p->mode > 2) return fail(ctx, DPG_ERR_INVALID_ARG, "bad mode");
+    const bool per_pid = p->mode == DPG_MODE_PER_PRIVACY_ID;
+    if (per_pid ? p->max_contributions <= 0
+                : (p->max_partitions_contributed <= 0 || p->max_contributions_per_partition <= 0))
+        return fail(ctx, DPG_ERR_INVALID_ARG, "contribution bounds must be positive");
+    if (n >= 0xFFFFFFFFll) return fail(ctx, DPG_ERR_UNSUPPORTED, "n must be < 2^32 per device");
+    const bool var = (p->metric_mask & (DPG_M_MEAN | DPG_M_VARIANCE)) != 0;
+    const bool need_values = (p->metric_mask & (DPG_M_SUM | DPG_M_MEAN | DPG_M_VARIANCE)) != 0;
+    if (need_values && n > 0 && !value)
+        return fail(ctx, DPG_ERR_INVALID_ARG, "value array required for SUM/MEAN/VARIANCE");
+    if (var && out->nsum == nullptr)
+        return fail(ctx, DPG_ERR_INVALID_ARG, "MEAN/VARIANCE need nsum/nsq partials");
+    if (need_values && !var && out->sum == nullptr)
+        return fail(ctx, DPG_ERR_INVALID_ARG, "SUM needs sum partials");
+    (void)hipSetDevice(ctx->device);
+    hipStream_t s = (hipStream_t)stream;
+    ctx->stage_names.clear();
+    ctx->n_events_used = 0;
+    ctx->last_stream = s;
+    int st = DPG_OK;
+    const int64_t P = p->n_partitions;
+    stage(ctx, s, "begin");
+    HIP_TRY(hipMemsetAsync(out->rows, 0, P * 8, s));
+    HIP_TRY(hipMemsetAsync(out->count, 0, P * 8, s));
+    if (out->sum) HIP_TRY(hipMemsetAsync(out->sum, 0, P * 8, s));
+    if (out->nsum) HIP_TRY(hipMemsetAsync(out->nsum, 0, P * 8, s));
+    if (out->nsq) HIP_TRY(hipMemsetAsync(out->nsq, 0, P * 8, s));
+    if (n == 0) return DPG_OK;
+
+    WS(ctl, Control, "control", 1);
+    HIP_TRY(hipMemsetAsync(ctl, 0, sizeof(Control), s));
+    {
+        Control h{};
+        h.n_scalar = n;
+        HIP_TRY(hipMemcpyAsync(&ctl->n_scalar, &h.n_scalar, 8, hipMemcpyHostToDevice, s));
+    }
+    WS(recA, Rec16, "recA", n);
+    WS(recB, Rec16, "recB", n);
+
+    // ---- level plan: total hash bits so buckets average ~kBucketTarget
+    uint32_t bits_total = std::max<uint32_t>(1, ceil_log2((double)n / kBucketTarget));
+    int levels = (int)((bits_total + 9) / 10);
+    if (levels > kMaxLevels) levels = kMaxLevels, bits_total = 10 * kMaxLevels;
+    uint32_t lbits[kMaxLevels] = {0, 0, 0};
+    for (int l = 0; l < levels; ++l) lbits[l] = bits_total / levels + (l < (int)(bits_total % levels));
+
+    Rec16 *cur = nullptr;
+    int64_t *bstart = nullptr;
+    uint32_t *bcnt = nullptr;
+    uint32_t S = 1;
+    uint32_t shift = 32;
+    for (int l = 0; l < levels; ++l) {
+        const uint32_t F = 1u << lbits[l];
+        shift -= lbits[l];
+        DigPid dig{shift, F - 1};
+        Rec16 *dst = (l % 2 == 0) ? recA : recB;
+        char tag[16];
+        std::snprintf(tag, sizeof(tag), "lvl%d", l);
+        stage(ctx, s, l == 0 ? "partition1" : (l == 1 ? "partition2" : "partition3"));
+        int r;
+        if (l == 0) {
+            SrcSoA src{pid, pk, need_values ? value : nullptr, p->public_mask, P, &ctl->err};
+            r = run_level<SrcSoA, Rec16, DigPid, kItemsPerThread>(
+                ctx, s, src, dig, 1u, nullptr, nullptr, &ctl->n_scalar, n, F, lbits[l], dst, tag,
+                &bstart, &bcnt, &ctl->ntiles[l]);
+        } else {
+            r = run_level<SrcAoS<Rec16>, Rec16, DigPid, kItemsPerThread>(
+                ctx, s, SrcAoS<Rec16>{cur}, dig, S, bstart, bcnt, nullptr, n, F, lbits[l], dst,
+                tag, &bstart, &bcnt, &ctl->ntiles[l]);
+        }
+        if (r) return r;
+        cur = dst;
+        S *= F;
+    }
+    const uint32_t B = S;
+    BoundParams bp = to_bound(p, ctx->seed);
+    Rec16 *other = (cur == recA) ? recB : recA;
+    if (!var) {
+        Item16 *items = reinterpret_cast<Item16 *>(other);
+        Item16 *items2 = reinterpret_cast<Item16 *>(cur);
+        return bound_and_reduce<Item16>(ctx, s, cur, bstart, bcnt, B, bp, items, items2, n, P, out,
+                                         ctl);
+    }
+    WS(it32a, Item32, "items32a", n);
+    WS(it32b, Item32, "items32b", n);
+    return bound_and_reduce<Item32>(ctx, s, cur, bstart, bcnt, B, bp, it32a, it32b, n, P, out, ctl);
+}
+
+int dpg_select_and_noise(dpg_ctx *ctx, const dpg_partials *in, const dpg_select_params *sel,
+                         const dpg_noise_params *z, uint8_t *keep, double *out, void *stream) {
+    if (!ctx) return DPG_ERR_INVALID_ARG;
+    if (!in || !sel || !z || !keep || (!out && z->n_outputs > 0))
+        return fail(ctx, DPG_ERR_INVALID_ARG, "null argument");
+    if (z->n_outputs < 0 || z->n_outputs > 8)
+        return fail(ctx, DPG_ERR_INVALID_ARG, "n_outputs must be in [0, 8]");
+    if (sel->strategy != DPG_SELECT_NONE && sel->max_rows_per_privacy_id <= 0)
+        return fail(ctx, DPG_ERR_INVALID_ARG, "max_rows_per_privacy_id must be positive");
+    (void)hipSetDevice(ctx->device);
+    hipStream_t s = (hipStream_t)stream;
+    int st = DPG_OK;
+    const int64_t P = in->n_partitions;
+    if (P <= 0) return DPG_OK;
+    SelectArgs a{};
+    a.strategy = sel->strategy;
+    a.table_len = sel->table_len;
+    a.threshold = sel->threshold;
+    a.noise_scale = sel->noise_scale;
+    a.pre_threshold = sel->pre_threshold;
+    a.max_rows = std::max<int64_t>(1, sel->max_rows_per_privacy_id);
+    a.pk_offset = sel->pk_offset;
+    a.public_mask = sel->public_mask;
+    a.table = nullptr;
+    if (sel->strategy == DPG_SELECT_TRUNCATED_GEOMETRIC) {
+        if (sel->table_len <= 0 || !sel->keep_table)
+            return fail(ctx, DPG_ERR_INVALID_ARG, "truncated geometric needs keep_table");
+        WS(tab, double, "select.table", sel->table_len);
+        HIP_TRY(hipMemcpyAsync(tab, sel->keep_table, sizeof(double) * sel->table_len,
+                               hipMemcpyHostToDevice, s));
+        a.table = tab;
+    }
+    NoiseArgs na{};
+    na.kind = z->noise_kind;
+    na.family = z->family;
+    na.slot_mask = z->slot_mask;
+    na.n_out = z->n_outputs;
+    for (int j = 0; j < 8; ++j) na.out_src[j] = std::min(4, std::max(0, z->out_src[j]));
+    for (int j = 0; j < 4; ++j) na.scale[j] = z->scale[j];
+    na.mid = z->mid;
+    na.mean_const = z->mean_const;
+    na.msq_const = z->msq_const;
+    na.mean_const_value = z->mean_const_value;
+    na.msq_const_value = z->msq_const_value;
+    const int threads = 256;
+    int64_t blocks = std::min<int64_t>((P + threads - 1) / threads, (int64_t)ctx->n_cu * 16);
+    size_t lds = (a.table && a.table_len <= 4096) ? (size_t)a.table_len * 8 : 0;
+    k_select_noise<<<(unsigned)blocks, threads, lds, s>>>(in->rows, in->count, in->sum, in->nsum,
+                                                         in->nsq, P, a, na, ctx->seed, keep, out);
+    LAUNCH_CHECK();
+    return DPG_OK;
+}
+
+int dpg_compact_kept(dpg_ctx *ctx, const uint8_t *keep, const double *out, int64_t P,
+                     int32_t n_out, int64_t *kept_ids, double *kept_out, int64_t *n_kept,
+                     void *stream) {
+    if (!ctx) return DPG_ERR_INVALID_ARG;
+    if (!keep || !kept_ids || !n_kept || (n_out > 0 && (!out || !kept_out)))
+        return fail(ctx, DPG_ERR_INVALID_ARG, "null argument");
+    (void)hipSetDevice(ctx->device);
+    hipStream_t s = (hipStream_t)stream;
+    int st = DPG_OK;
+    if (P <= 0) {
+        *n_kept = 0;
+        return DPG_OK;
+    }
+    uint32_t nb = (uint32_t)((P + kCompactPerBlock - 1) / kCompactPerBlock);
+    WS(bc, uint32_t, "compact.blocks", nb);
+    WS(tot, int64_t, "compact.total", 1);
+    k_compact_count<<<nb, kCompactThreads, 0, s>>>(keep, P, bc);
+    LAUNCH_CHECK();
+    k_compact_scan<<<1, 1024, 0, s>>>(bc, nb, tot);
+    LAUNCH_CHECK();
+    k_compact_write<<<nb, kCompactThreads, 0, s>>>(keep, out, P, n_out, bc, kept_ids, kept_out);
+    LAUNCH_CHECK();
+    HIP_TRY(hipMemcpyAsync(n_kept, tot, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return DPG_OK;
+}
+
+int dpg_last_stage_times(dpg_ctx *ctx, char *names, size_t names_len, double *ms,
+                         int32_t max_stages, int32_t *n_stages) {
+    if (!ctx || !n_stages) return DPG_ERR_INVALID_ARG;
+    int ns = ctx->n_events_used - 1;
+    if (ns < 0) ns = 0;
+    if (ns > max_stages) ns = max_stages;
+    *n_stages = ns;
+    if (ns == 0) return DPG_OK;
+    (void)hipEventSynchronize(ctx->events[ctx->n_events_used - 1]);
+    std::string joined;
+    for (int i = 0; i < ns; ++i) {
+        float t = 0.f;
+        (void)hipEventElapsedTime(&t, ctx->events[i], ctx->events[i + 1]);
+        if (ms) ms[i] = t;
+        if (i) joined += ",";
+        joined += ctx->stage_names[i];
+    }
+    if (names && names_len) std::snprintf(names, names_len, "%s", joined.c_str());
+    return DPG_OK;
+}
+
+}  // extern "C"

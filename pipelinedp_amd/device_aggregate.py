@@ -1,0 +1,197 @@
+"""Lazy device execution of one DPEngine.aggregate / select_partitions call.
+
+The reference returns a lazy collection whose generators run when the user
+iterates it, after `BudgetAccountant.compute_budgets()` (SURVEY.md 3.4;
+pinned by the reference's tests/pipeline_backend_test.py:564-591).  This
+object keeps that contract: nothing touches the GPU until the first
+`__iter__` / `materialize()`, and budgets are read at that moment.
+
+Device pipeline per call (include/dpg.h):
+  dpg_bound_aggregate -> [multi-GPU: reduce-scatter of the dense partials]
+  -> dpg_select_and_noise -> dpg_compact_kept.
+"""
+import ctypes
+import dataclasses
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from pipelinedp_amd import _native
+from pipelinedp_amd import columnar
+from pipelinedp_amd import combiners
+from pipelinedp_amd import distributed
+from pipelinedp_amd import partition_selection
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+@dataclasses.dataclass
+class DeviceResult:
+    """Materialised result: kept partition ids and their metric columns, on the
+    device.  `keys()` maps ids back to the user's partition keys."""
+    partition_ids: torch.Tensor        # int64 [K] (global dense ids)
+    values: torch.Tensor               # float64 [K, len(fields)]
+    fields: tuple
+    key_table: Optional[Sequence]
+    stage_ms: dict = dataclasses.field(default_factory=dict)
+
+    def keys(self) -> list:
+        return columnar.decode_keys(self.partition_ids.cpu().numpy(), self.key_table)
+
+
+class DeviceAggregation:
+    """Lazy collection of (partition_key, MetricsTuple) -- or of partition
+    keys for select_partitions."""
+
+    def __init__(self, backend, col, extractors, plan: Optional[combiners.CompoundPlan],
+                 public_partitions=None, selection_spec=None, strategy=None,
+                 max_partitions_contributed: int = 1, pre_threshold=None,
+                 max_rows_per_privacy_id: int = 1, drop_non_public: bool = True,
+                 bounds_already_enforced: bool = False, keys_only: bool = False):
+        self.backend = backend
+        self.col = col
+        self.extractors = extractors
+        self.plan = plan
+        self.public_partitions = public_partitions
+        self.selection_spec = selection_spec
+        self.strategy = strategy
+        self.max_partitions_contributed = max_partitions_contributed
+        self.pre_threshold = pre_threshold
+        self.max_rows = max_rows_per_privacy_id
+        self.drop_non_public = drop_non_public
+        self.bounds_already_enforced = bounds_already_enforced
+        self.keys_only = keys_only
+        self._result: Optional[DeviceResult] = None
+        self.last_partials = None
+        self.noise_enabled = True
+
+    # ------------------------------------------------------------ public
+    def __iter__(self):
+        res = self.materialize()
+        keys = res.keys()
+        if self.keys_only:
+            return iter(keys)
+        vals = res.values.cpu().numpy()
+        T = self.plan.MetricsTuple
+        return iter([(k, T(*map(float, row))) for k, row in zip(keys, vals)])
+
+    def materialize(self, gather: bool = True) -> DeviceResult:
+        if self._result is None:
+            self._result = self._run(gather)
+        return self._result
+
+    # ------------------------------------------------------------ device
+    def _bound_fields(self, P: int) -> dict:
+        if self.plan is not None:
+            f = self.plan.bound_fields(P)
+        else:  # select_partitions: cross-partition bounding, keys only
+            f = dict(mode=combiners.MODE_CROSS, sum_mode=combiners.SUM_NONE, metric_mask=0,
+                     max_partitions_contributed=self.max_partitions_contributed,
+                     max_contributions_per_partition=1, max_contributions=0,
+                     min_value=0.0, max_value=0.0, min_sum_per_partition=0.0,
+                     max_sum_per_partition=0.0, n_partitions=P)
+        if self.bounds_already_enforced:
+            # every row is its own privacy unit: bounding never samples
+            f.update(mode=combiners.MODE_CROSS_AND_PER if f["mode"] != combiners.MODE_CROSS
+                     else combiners.MODE_CROSS,
+                     max_partitions_contributed=max(1, f["max_partitions_contributed"]),
+                     max_contributions_per_partition=max(1, f["max_contributions_per_partition"]))
+            if f["mode"] == combiners.MODE_PER_PID:
+                f["mode"] = combiners.MODE_CROSS_AND_PER
+        return f
+
+    def _select_fields(self, pk_offset: int, public_mask_local) -> dict:
+        if self.public_partitions is not None:
+            return dict(strategy=0, table_len=0, keep_table=None, threshold=0.0,
+                        noise_scale=0.0, pre_threshold=0, max_rows_per_privacy_id=1,
+                        pk_offset=pk_offset, public_mask=public_mask_local)
+        spec = self.selection_spec
+        sp = partition_selection.create_partition_selection_strategy(
+            self.strategy, spec.eps, spec.delta, self.max_partitions_contributed,
+            self.pre_threshold)
+        self._selection_plan = sp
+        f = dict(strategy=sp.native_strategy, table_len=0, keep_table=None,
+                 threshold=sp.threshold, noise_scale=sp.noise_scale,
+                 pre_threshold=int(self.pre_threshold or 0),
+                 max_rows_per_privacy_id=int(self.max_rows), pk_offset=pk_offset,
+                 public_mask=None)
+        if sp.table is not None:
+            self._table = np.ascontiguousarray(np.asarray(sp.table, dtype=np.float64))
+            f["table_len"] = len(self._table)
+            f["keep_table"] = self._table.ctypes.data
+        return f
+
+    def _run(self, gather: bool) -> DeviceResult:
+        backend = self.backend
+        ctx = backend.ctx
+        dev = backend.device
+        need_values = self.plan is not None and self.plan.needs_values()
+        enc = columnar.encode(self.col, self.extractors, dev, need_values,
+                              self.public_partitions,
+                              need_pid=not self.bounds_already_enforced)
+        if self.bounds_already_enforced:
+            enc.pid = torch.arange(enc.n, dtype=torch.int64, device=dev)
+        # noise / selection parameters are resolved now (after compute_budgets)
+        noise = (self.plan.noise_fields(self.noise_enabled) if self.plan is not None else
+                 dict(noise_kind=0, family=0, slot_mask=0, n_outputs=0, out_src=[0] * 8,
+                      scale=[0.0] * 4, mid=0.0, mean_const=0, msq_const=0,
+                      mean_const_value=0.0, msq_const_value=0.0))
+        P = enc.n_partitions
+        with torch.cuda.device(dev):
+            stream = torch.cuda.current_stream(dev)
+            sptr = ctypes.c_void_p(stream.cuda_stream)
+            f64 = dict(dtype=torch.float64, device=dev)
+            rows = torch.empty(P, dtype=torch.int64, device=dev)
+            count = torch.empty(P, dtype=torch.int64, device=dev)
+            mask = self.plan.mask if self.plan is not None else 0
+            sum_ = torch.empty(P, **f64) if mask & combiners.M_SUM else None
+            var = mask & (combiners.M_MEAN | combiners.M_VARIANCE)
+            nsum = torch.empty(P, **f64) if var else None
+            nsq = torch.empty(P, **f64) if var else None
+            bfields = self._bound_fields(P)
+            bound = _native.fill(_native.BoundParams, bfields)
+            if enc.public_mask is not None and self.drop_non_public:
+                bound.public_mask = enc.public_mask.data_ptr()
+            partials = _native.Partials(P, rows.data_ptr(), count.data_ptr(),
+                                        sum_.data_ptr() if sum_ is not None else None,
+                                        nsum.data_ptr() if nsum is not None else None,
+                                        nsq.data_ptr() if nsq is not None else None)
+            ctx.bound_aggregate(_ptr(enc.pid), _ptr(enc.pk),
+                                _ptr(enc.value) if need_values else None,
+                                enc.n, bound, partials, sptr)
+            stage_ms = {}
+            tensors = dict(rows=rows, count=count, sum=sum_, nsum=nsum, nsq=nsq)
+            self.last_partials = tensors
+            pk_offset, local_P = 0, P
+            public_mask_local = enc.public_mask
+            if backend.world_size > 1:
+                tensors, pk_offset, local_P = distributed.reduce_scatter_partials(
+                    tensors, P, backend.process_group)
+                if public_mask_local is not None:
+                    public_mask_local = distributed.slice_bitmap(
+                        enc.public_mask, pk_offset, local_P)
+            lp = _native.Partials(local_P, tensors["rows"].data_ptr(),
+                                  tensors["count"].data_ptr(),
+                                  *(tensors[k].data_ptr() if tensors[k] is not None else None
+                                    for k in ("sum", "nsum", "nsq")))
+            sfields = self._select_fields(
+                pk_offset, public_mask_local.data_ptr() if public_mask_local is not None else None)
+            sel = _native.fill(_native.SelectParams, sfields)
+            nz = _native.fill(_native.NoiseParams, noise)
+            n_out = noise["n_outputs"]
+            keep = torch.empty(local_P, dtype=torch.uint8, device=dev)
+            out = torch.empty(max(local_P * n_out, 1), **f64)
+            ctx.select_and_noise(lp, sel, nz, keep.data_ptr(), out.data_ptr(), sptr)
+            ids = torch.empty(local_P, dtype=torch.int64, device=dev)
+            kept_out = torch.empty(max(local_P * n_out, 1), **f64)
+            k = ctx.compact(keep.data_ptr(), out.data_ptr(), local_P, n_out, ids.data_ptr(),
+                            kept_out.data_ptr(), sptr)
+            ids = ids[:k] + pk_offset
+            vals = kept_out[:k * n_out].view(k, n_out) if n_out else torch.empty((k, 0), **f64)
+            if backend.world_size > 1 and gather:
+                ids, vals = distributed.all_gather_results(ids, vals, backend.process_group)
+        fields = self.plan.fields if self.plan is not None else ()
+        return DeviceResult(ids, vals, fields, enc.key_table, stage_ms)
