@@ -151,12 +151,19 @@ typedef struct dpg_noise_params {
 
 typedef struct dpg_ctx dpg_ctx;
 
-/* Context: device ordinal, 128-bit... (64-bit) seed of every keyed random
- * stream. Returns NULL on failure. */
+/* Context: device ordinal and the 64-bit seed of every keyed random stream.
+ * Returns NULL on failure. */
 dpg_ctx *dpg_ctx_create(int device, uint64_t seed);
 void dpg_ctx_destroy(dpg_ctx *ctx);
 int dpg_last_error(dpg_ctx *ctx, char *buf, size_t len);
 int dpg_set_seed(dpg_ctx *ctx, uint64_t seed);
+
+/* Tuning / testing hook: average records per privacy-id bucket the
+ * partition levels aim for (default 1024; smaller values force more levels
+ * on small inputs) and the largest bucket processed in LDS (default and
+ * maximum 2048; larger buckets take the global-memory path).  <= 0 keeps
+ * the current value. */
+int dpg_set_tuning(dpg_ctx *ctx, int32_t bucket_target, int32_t bucket_cap);
 
 /* Contribution bounding + per-(pid,pk) accumulators + merge per partition.
  * pid, pk: device int64[n]; value: device double[n] or NULL (COUNT / PID

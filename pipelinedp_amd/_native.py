@@ -15,6 +15,7 @@ ERRORS = {1: "invalid argument", 2: "key out of range", 3: "HIP error",
           4: "out of device memory", 5: "unsupported"}
 
 EXPORTED = ("dpg_ctx_create", "dpg_ctx_destroy", "dpg_last_error", "dpg_set_seed",
+            "dpg_set_tuning",
             "dpg_bound_aggregate", "dpg_select_and_noise", "dpg_compact_kept",
             "dpg_last_stage_times")
 
@@ -99,6 +100,8 @@ def load():
         lib.dpg_last_error.restype = ctypes.c_int
         lib.dpg_set_seed.argtypes = [vp, ctypes.c_uint64]
         lib.dpg_set_seed.restype = ctypes.c_int
+        lib.dpg_set_tuning.argtypes = [vp, i32, i32]
+        lib.dpg_set_tuning.restype = ctypes.c_int
         lib.dpg_bound_aggregate.argtypes = [vp, vp, vp, vp, i64,
                                             ctypes.POINTER(BoundParams),
                                             ctypes.POINTER(Partials), vp]
@@ -152,6 +155,10 @@ class Context:
     def set_seed(self, seed: int):
         self.check(self.lib.dpg_set_seed(self.handle, ctypes.c_uint64(seed & (2**64 - 1))),
                    "dpg_set_seed")
+
+    def set_tuning(self, bucket_target: int = 0, bucket_cap: int = 0):
+        self.check(self.lib.dpg_set_tuning(self.handle, int(bucket_target), int(bucket_cap)),
+                   "dpg_set_tuning")
 
     def bound_aggregate(self, pid_ptr, pk_ptr, value_ptr, n, bound: BoundParams,
                         partials: Partials, stream):

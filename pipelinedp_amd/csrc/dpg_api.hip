@@ -8,6 +8,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdlib>
+#include <thread>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -57,9 +60,43 @@ struct dpg_ctx {
     std::vector<hipEvent_t> events;
     int n_events_used = 0;
     hipStream_t last_stream = nullptr;
+    uint32_t bucket_target = kBucketTarget;
+    uint32_t bucket_cap = kBucketCap;
 };
 
 namespace {
+
+// Debug watchdog (env DPG_WATCHDOG_S=<seconds>): instead of blocking, poll
+// the stream; on timeout print each workgroup's last phase and abort.
+int watchdog_seconds() {
+    const char *e = std::getenv("DPG_WATCHDOG_S");
+    return e ? std::atoi(e) : 0;
+}
+
+uint32_t *watchdog_buffer(size_t n) {
+    static uint32_t *buf = nullptr;
+    static size_t cap = 0;
+    if (n > cap) {
+        if (buf) (void)hipHostFree(buf);
+        if (hipHostMalloc((void **)&buf, n * 4, hipHostMallocCoherent) != hipSuccess) return nullptr;
+        cap = n;
+    }
+    std::memset(buf, 0, n * 4);
+    return buf;
+}
+
+void watchdog_wait(hipStream_t s, const uint32_t *prog, size_t n, const char *what) {
+    int secs = watchdog_seconds();
+    for (int i = 0; i < secs * 100; ++i) {
+        if (hipStreamQuery(s) == hipSuccess) return;
+        std::this_thread::sleep_for(std::chrono::milliseconds(10));
+    }
+    std::fprintf(stderr, "[dpg watchdog] %s did not finish in %d s; phases:", what, secs);
+    for (size_t i = 0; i < n; ++i) std::fprintf(stderr, " %u", prog[i]);
+    std::fprintf(stderr, "\n");
+    std::fflush(stderr);
+    std::abort();
+}
 
 int fail(dpg_ctx *c, int code, const std::string &msg) {
     if (c) c->err = msg;
@@ -176,19 +213,29 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Rec16 *recs, const int64
                      Item *items2, int64_t n, int64_t P, const dpg_partials *out, Control *ctl) {
     int st = DPG_OK;
     WS(oversize, uint32_t, "bound.oversize", B);
+    WS(oflag, uint8_t, "bound.oflag", B);
+    HIP_TRY(hipMemsetAsync(oflag, 0, B, s));
     const size_t lds = BucketLayout::make(kBucketCap, ItemTraits<Item>::var, 2).total +
                        align16(sizeof(BucketShared));
     stage(ctx, s, "bound");
-    k_bound_lds<Item><<<ctx->n_cu, kBoundThreads, lds, s>>>(
-        recs, bstart, bcnt, B, kBucketCap, &ctl->queue, bp, items, &ctl->item_cursor, oversize,
-        &ctl->n_oversize);
+    BoundParams bpl = bp;
+    uint32_t *prog = watchdog_seconds() ? watchdog_buffer(ctx->n_cu) : nullptr;
+    bpl.progress = prog;
+    k_bound_lds<Item><<<ctx->n_cu, kBoundThreads, lds, s>>>(recs, bstart, bcnt, B, ctx->bucket_cap,
+                                                            bpl, items, &ctl->item_cursor, oflag);
+    LAUNCH_CHECK();
+    if (prog) watchdog_wait(s, prog, ctx->n_cu, "k_bound_lds");
+    k_collect_flags<<<std::min<uint32_t>((B + 255) / 256, 1024), 256, 0, s>>>(oflag, B, oversize,
+                                                                               &ctl->n_oversize);
     LAUNCH_CHECK();
     // oversize buckets (rare): global-memory working sets
     Control hctl;
     HIP_TRY(hipMemcpyAsync(&hctl, ctl, sizeof(Control), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    if (hctl.err) return fail(ctx, DPG_ERR_KEY_RANGE,
-                              "privacy id outside [0, 2^32-1) or partition key outside [0, P)");
+    if (hctl.err & 1u)
+        return fail(ctx, DPG_ERR_KEY_RANGE,
+                    "privacy id outside [0, 2^32-1) or partition key outside [0, P)");
+    if (hctl.err & 2u) return fail(ctx, DPG_ERR_HIP, "internal hash-table error in bounding");
     if (hctl.n_oversize > 0) {
         const uint32_t no = hctl.n_oversize;
         std::vector<uint32_t> list(no), cnt(B);
@@ -203,9 +250,18 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Rec16 *recs, const int64
         WS(scratch, char, "bound.scratch", total);
         WS(doff, size_t, "bound.scratch_off", no);
         HIP_TRY(hipMemcpyAsync(doff, off.data(), no * sizeof(size_t), hipMemcpyHostToDevice, s));
+        BoundParams bpg = bp;
+        uint32_t *gprog = watchdog_seconds() ? watchdog_buffer(no) : nullptr;
+        bpg.progress = gprog;
+        if (watchdog_seconds())
+            std::fprintf(stderr, "[dpg] %u oversize buckets, scratch %zu bytes\n", no, total);
         k_bound_global<Item><<<no, kBoundThreads, 0, s>>>(recs, bstart, bcnt, oversize, doff,
-                                                          scratch, bp, items, &ctl->item_cursor);
+                                                          scratch, bpg, items, &ctl->item_cursor);
         LAUNCH_CHECK();
+        if (gprog) watchdog_wait(s, gprog, no, "k_bound_global");
+        HIP_TRY(hipMemcpyAsync(&hctl, ctl, sizeof(Control), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (hctl.err & 2u) return fail(ctx, DPG_ERR_HIP, "internal hash-table error (global path)");
     }
     // ---- merge kept pairs per partition
     stage(ctx, s, "reduce");
@@ -280,6 +336,13 @@ int dpg_set_seed(dpg_ctx *c, uint64_t seed) {
     return DPG_OK;
 }
 
+int dpg_set_tuning(dpg_ctx *ctx, int32_t bucket_target, int32_t bucket_cap) {
+    if (!ctx) return DPG_ERR_INVALID_ARG;
+    if (bucket_target > 0) ctx->bucket_target = (uint32_t)bucket_target;
+    if (bucket_cap > 0) ctx->bucket_cap = std::min<uint32_t>((uint32_t)bucket_cap, kBucketCap);
+    return DPG_OK;
+}
+
 int dpg_bound_aggregate(dpg_ctx *ctx, const int64_t *pid, const int64_t *pk, const double *value,
                         int64_t n, const dpg_bound_params *p, dpg_partials *out, void *stream) {
     if (!ctx) return DPG_ERR_INVALID_ARG;
@@ -329,7 +392,7 @@ int dpg_bound_aggregate(dpg_ctx *ctx, const int64_t *pid, const int64_t *pk, con
     WS(recB, Rec16, "recB", n);
 
     // ---- level plan: total hash bits so buckets average ~kBucketTarget
-    uint32_t bits_total = std::max<uint32_t>(1, ceil_log2((double)n / kBucketTarget));
+    uint32_t bits_total = std::max<uint32_t>(1, ceil_log2((double)n / ctx->bucket_target));
     int levels = (int)((bits_total + 9) / 10);
     if (levels > kMaxLevels) levels = kMaxLevels, bits_total = 10 * kMaxLevels;
     uint32_t lbits[kMaxLevels] = {0, 0, 0};
@@ -365,6 +428,8 @@ int dpg_bound_aggregate(dpg_ctx *ctx, const int64_t *pid, const int64_t *pk, con
     }
     const uint32_t B = S;
     BoundParams bp = to_bound(p, ctx->seed);
+    bp.err = &ctl->err;
+    bp.progress = nullptr;
     Rec16 *other = (cur == recA) ? recB : recA;
     if (!var) {
         Item16 *items = reinterpret_cast<Item16 *>(other);

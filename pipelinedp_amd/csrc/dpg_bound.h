@@ -37,7 +37,15 @@ struct BoundParams {
     uint32_t mpc, mcpp, L;
     double lo, hi, lo_pp, hi_pp, mid;
     uint64_t seed;
+    uint32_t *err;       // bit 1: internal table error
+    uint32_t *progress;  // debug watchdog: last phase per workgroup (or null)
 };
+
+__device__ __forceinline__ void mark(const BoundParams &bp, uint32_t phase) {
+    if (bp.progress && threadIdx.x == 0)
+        __hip_atomic_store(&bp.progress[blockIdx.x], phase, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 __host__ __device__ __forceinline__ uint32_t next_pow2(uint32_t x) {
     uint32_t p = 64;
@@ -87,27 +95,52 @@ __device__ __forceinline__ uint32_t hslot64(uint64_t key, uint32_t mask) {
     return fmix32((uint32_t)key ^ fmix32((uint32_t)(key >> 32) + 0x7F4A7C15u)) & mask;
 }
 
-__device__ __forceinline__ uint32_t insert32(uint32_t *keys, uint32_t mask, uint32_t key) {
+// Probe loops are bounded by the table size: a miss after a full sweep can
+// only be a bug, which is reported through *err instead of spinning.
+__device__ __forceinline__ uint32_t insert32(uint32_t *keys, uint32_t mask, uint32_t key,
+                                             uint32_t *err) {
     uint32_t h = hslot32(key, mask);
-    while (true) {
+    for (uint32_t probe = 0; probe <= mask; ++probe) {
         uint32_t old = atomicCAS(&keys[h], kEmpty32, key);
         if (old == kEmpty32 || old == key) return h;
         h = (h + 1) & mask;
     }
+    atomicOr(err, 2u);
+    return 0;
 }
-__device__ __forceinline__ uint32_t lookup32(const uint32_t *keys, uint32_t mask, uint32_t key) {
+__device__ __forceinline__ uint32_t lookup32(const uint32_t *keys, uint32_t mask, uint32_t key,
+                                             uint32_t *err) {
     uint32_t h = hslot32(key, mask);
-    while (keys[h] != key) h = (h + 1) & mask;
-    return h;
+    for (uint32_t probe = 0; probe <= mask; ++probe) {
+        if (keys[h] == key) return h;
+        h = (h + 1) & mask;
+    }
+    atomicOr(err, 2u);
+    return 0;
 }
-__device__ __forceinline__ uint32_t insert64(uint64_t *keys, uint32_t mask, uint64_t key) {
+__device__ __forceinline__ uint32_t insert64(uint64_t *keys, uint32_t mask, uint64_t key,
+                                             uint32_t *err) {
     uint32_t h = hslot64(key, mask);
-    while (true) {
+    for (uint32_t probe = 0; probe <= mask; ++probe) {
         uint64_t old = atomicCAS((unsigned long long *)&keys[h], (unsigned long long)kEmpty64,
                                  (unsigned long long)key);
         if (old == kEmpty64 || old == key) return h;
         h = (h + 1) & mask;
     }
+    atomicOr(err, 2u);
+    return 0;
+}
+
+// Workgroup barrier of a bucket pass.  With the working set in global memory
+// (oversize buckets) the tables are written by L2 atomics and plain stores
+// and re-read by plain loads, so each wave drops this CU's possibly stale L1
+// lines after the barrier (agent-scope acquire, MI355X_MICROARCH.md
+// "inter-workgroup visibility"); in LDS the plain barrier suffices.
+template <bool kGlobal>
+__device__ __forceinline__ void bucket_sync() {
+    if (kGlobal) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __syncthreads();
+    if (kGlobal) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 }
 
 // keep-the-k-smallest-distinct cascade (slot values only decrease)
@@ -123,7 +156,7 @@ __device__ __forceinline__ void cascade_insert(uint64_t *slots, uint32_t k, uint
 }
 
 // Block compaction: dense id for every flagged slot in [0, C).  Returns count.
-template <class Idx>
+template <bool kGlobal, class Idx>
 __device__ __forceinline__ uint32_t block_enumerate(uint32_t C, const uint32_t *keys32,
                                                    const uint64_t *keys64, Idx *s2i,
                                                    uint32_t *sh16, uint32_t *sh_total) {
@@ -135,7 +168,7 @@ __device__ __forceinline__ uint32_t block_enumerate(uint32_t C, const uint32_t *
         if (s < C) occ = keys32 ? keys32[s] != kEmpty32 : keys64[s] != kEmpty64;
         uint64_t bal = __ballot(occ);
         if (lane == 0) sh16[w] = __popcll(bal);
-        __syncthreads();
+        bucket_sync<kGlobal>();
         uint32_t pre = 0, tot = 0;
         for (int k = 0; k < 16; ++k) {
             uint32_t y = sh16[k];
@@ -144,7 +177,7 @@ __device__ __forceinline__ uint32_t block_enumerate(uint32_t C, const uint32_t *
         }
         if (occ) s2i[s] = (Idx)(running + pre + __popcll(bal & ((1ull << lane) - 1ull)));
         running += tot;
-        __syncthreads();
+        bucket_sync<kGlobal>();
     }
     if (tid == 0) *sh_total = running;
     return running;
@@ -162,10 +195,12 @@ __device__ __forceinline__ void process_bucket(const Rec16 *__restrict__ recs, u
                                                const BoundParams &bp, Item *items,
                                                uint32_t *item_cursor) {
     constexpr bool kVar = ItemTraits<Item>::var;
+    constexpr bool kGlobal = sizeof(Idx) == 4;
+    uint32_t *err = bp.err;
     const int tid = threadIdx.x;
     const BucketLayout L = BucketLayout::make(n, kVar, (int)sizeof(Idx));
     const uint32_t nilI = (uint32_t)(Idx)(~0u);
-    const uint32_t C = L.C, cmask = C - 1;
+    const uint32_t C = __builtin_amdgcn_readfirstlane(L.C), cmask = C - 1;
     // T region (tables; reused in D/E)
     uint32_t *pidkey = reinterpret_cast<uint32_t *>(base + L.t_off);
     uint64_t *pairkey = reinterpret_cast<uint64_t *>(base + L.t_off + (size_t)C * 4);
@@ -202,17 +237,19 @@ __device__ __forceinline__ void process_bucket(const Rec16 *__restrict__ recs, u
         pid_n[i] = 0;
     }
     if (tid == 0) sh->bump = 0;
-    __syncthreads();
+    bucket_sync<kGlobal>();
+    mark(bp, 1);
     // ---- A1: hash inserts
     for (uint32_t i = tid; i < n; i += kBoundThreads) {
         Rec16 r = recs[i];
-        insert32(pidkey, cmask, r.pid);
-        rec_pair[i] = (Idx)insert64(pairkey, cmask, ((uint64_t)r.pid << 32) | r.pk);
+        insert32(pidkey, cmask, r.pid, err);
+        rec_pair[i] = (Idx)insert64(pairkey, cmask, ((uint64_t)r.pid << 32) | r.pk, err);
     }
-    __syncthreads();
+    bucket_sync<kGlobal>();
+    mark(bp, 2);
     // ---- A2: dense ids
-    const uint32_t npid = block_enumerate(C, pidkey, nullptr, pid_s2i, sh->sh16, &sh->npid);
-    const uint32_t npair = block_enumerate(C, nullptr, pairkey, pair_s2i, sh->sh16, &sh->npair);
+    const uint32_t npid = block_enumerate<kGlobal>(C, pidkey, nullptr, pid_s2i, sh->sh16, &sh->npid);
+    const uint32_t npair = block_enumerate<kGlobal>(C, nullptr, pairkey, pair_s2i, sh->sh16, &sh->npair);
     for (uint32_t s = tid; s < C; s += kBoundThreads) {
         uint32_t k = pidkey[s];
         if (k != kEmpty32) pid_val[pid_s2i[s]] = k;
@@ -220,10 +257,11 @@ __device__ __forceinline__ void process_bucket(const Rec16 *__restrict__ recs, u
         if (pk2 != kEmpty64) {
             uint32_t id = pair_s2i[s];
             pair_pk[id] = (uint32_t)pk2;
-            pair_pid[id] = pid_s2i[lookup32(pidkey, cmask, (uint32_t)(pk2 >> 32))];
+            pair_pid[id] = pid_s2i[lookup32(pidkey, cmask, (uint32_t)(pk2 >> 32), err)];
         }
     }
-    __syncthreads();
+    bucket_sync<kGlobal>();
+    mark(bp, 3);
     // ---- A3: counts and lists
     const bool per_pid = bp.mode == DPG_MODE_PER_PRIVACY_ID;
     for (uint32_t i = tid; i < n; i += kBoundThreads) {
@@ -235,13 +273,14 @@ __device__ __forceinline__ void process_bucket(const Rec16 *__restrict__ recs, u
     }
     if (!per_pid)
         for (uint32_t p = tid; p < npair; p += kBoundThreads) atomicAdd(&pid_n[pair_pid[p]], 1u);
-    __syncthreads();  // tables dead from here on
+    bucket_sync<kGlobal>();  // tables dead from here on
 
     // ---- stage values (needed by D and E)
     if (bp.need_values)
         for (uint32_t i = tid; i < n; i += kBoundThreads) vstage[i] = recs[i].v;
 
     if (!per_pid) {
+        mark(bp, 4);
         // ---- C: cross-partition (mpc) selection over pairs
         for (uint32_t q = tid; q < npid; q += kBoundThreads) {
             uint32_t s = kNil;
@@ -251,7 +290,7 @@ __device__ __forceinline__ void process_bucket(const Rec16 *__restrict__ recs, u
             }
             pid_slot[q] = s;
         }
-        __syncthreads();
+        bucket_sync<kGlobal>();
         for (uint32_t p = tid; p < npair; p += kBoundThreads) {
             uint32_t q = pair_pid[p];
             if (pid_slot[q] != kNil) {
@@ -260,7 +299,7 @@ __device__ __forceinline__ void process_bucket(const Rec16 *__restrict__ recs, u
                 cascade_insert(slots + pid_slot[q], bp.mpc, key);
             }
         }
-        __syncthreads();
+        bucket_sync<kGlobal>();
         for (uint32_t p = tid; p < npair; p += kBoundThreads) {
             uint32_t q = pair_pid[p];
             bool kept = true;
@@ -271,9 +310,10 @@ __device__ __forceinline__ void process_bucket(const Rec16 *__restrict__ recs, u
             }
             pair_state[p] = kept ? kKeptAll : kDropped;
         }
-        __syncthreads();
+        bucket_sync<kGlobal>();
         if (tid == 0) sh->bump = 0;
-        __syncthreads();
+        bucket_sync<kGlobal>();
+        mark(bp, 5);
         // ---- D: per-partition (mcpp) sampling inside kept pairs
         const bool sample = bp.mode == DPG_MODE_CROSS_AND_PER_PARTITION && bp.need_values;
         if (sample) {
@@ -284,7 +324,7 @@ __device__ __forceinline__ void process_bucket(const Rec16 *__restrict__ recs, u
                     pair_state[p] = s;
                 }
             }
-            __syncthreads();
+            bucket_sync<kGlobal>();
             for (uint32_t i = tid; i < n; i += kBoundThreads) {
                 uint32_t p = rec_pair[i];
                 uint32_t st = pair_state[p];
@@ -301,7 +341,7 @@ __device__ __forceinline__ void process_bucket(const Rec16 *__restrict__ recs, u
                     cascade_insert(slots + st, bp.mcpp, key);
                 }
             }
-            __syncthreads();
+            bucket_sync<kGlobal>();
         }
         // kept flag per record -> rec_next
         for (uint32_t i = tid; i < n; i += kBoundThreads) {
@@ -310,7 +350,7 @@ __device__ __forceinline__ void process_bucket(const Rec16 *__restrict__ recs, u
             if (sample && st < kKeptAll) k = rkey[i] <= slots[st + bp.mcpp - 1];
             rec_next[i] = k ? 1 : 0;
         }
-        __syncthreads();
+        bucket_sync<kGlobal>();
     } else {
         // ---- PER_PRIVACY_ID: keep the L records of each pid with the
         // smallest record key (pid_n holds the pid's record count)
@@ -322,7 +362,7 @@ __device__ __forceinline__ void process_bucket(const Rec16 *__restrict__ recs, u
             }
             pid_slot[q] = s;
         }
-        __syncthreads();
+        bucket_sync<kGlobal>();
         for (uint32_t i = tid; i < n; i += kBoundThreads) {
             uint32_t p = rec_pair[i];
             uint32_t q = pair_pid[p];
@@ -341,9 +381,9 @@ __device__ __forceinline__ void process_bucket(const Rec16 *__restrict__ recs, u
                 cascade_insert(slots + pid_slot[q], bp.L, key);
             }
         }
-        __syncthreads();
+        bucket_sync<kGlobal>();
         for (uint32_t p = tid; p < npair; p += kBoundThreads) pair_head[p] = 0;  // kept count
-        __syncthreads();
+        bucket_sync<kGlobal>();
         for (uint32_t i = tid; i < n; i += kBoundThreads) {
             uint32_t p = rec_pair[i];
             uint32_t q = pair_pid[p];
@@ -351,9 +391,10 @@ __device__ __forceinline__ void process_bucket(const Rec16 *__restrict__ recs, u
             rec_next[i] = k ? 1 : 0;
             if (k) atomicAdd(&pair_head[p], 1u);
         }
-        __syncthreads();
+        bucket_sync<kGlobal>();
     }
 
+    mark(bp, 6);
     // ---- E: accumulators of kept records (slots/rkey dead; acc overlays)
     const bool part_clip = bp.sum_mode == DPG_SUM_CLIP_PARTITION;
     if (bp.need_values) {
@@ -364,7 +405,7 @@ __device__ __forceinline__ void process_bucket(const Rec16 *__restrict__ recs, u
                 acc_nsq[p] = 0.0;
             }
         }
-        __syncthreads();
+        bucket_sync<kGlobal>();
         for (uint32_t i = tid; i < n; i += kBoundThreads) {
             if (!rec_next[i]) continue;
             uint32_t p = rec_pair[i];
@@ -381,8 +422,9 @@ __device__ __forceinline__ void process_bucket(const Rec16 *__restrict__ recs, u
                 }
             }
         }
-        __syncthreads();
+        bucket_sync<kGlobal>();
     }
+    mark(bp, 7);
     // ---- F: emit kept pairs
     uint32_t kept_here = 0;
     for (uint32_t p = tid; p < npair; p += kBoundThreads) {
@@ -399,14 +441,14 @@ __device__ __forceinline__ void process_bucket(const Rec16 *__restrict__ recs, u
         uint32_t x = kept_here;
         for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
         if (lane == 0) sh->sh16[w] = x;
-        __syncthreads();
+        bucket_sync<kGlobal>();
         if (tid == 0) {
             uint32_t tot = 0;
             for (int k = 0; k < 16; ++k) tot += sh->sh16[k];
             sh->item_base = tot ? atomicAdd(item_cursor, tot) : 0;
             sh->nkept = 0;
         }
-        __syncthreads();
+        bucket_sync<kGlobal>();
     }
     for (uint32_t p = tid; p < npair; p += kBoundThreads) {
         uint32_t c;
@@ -431,32 +473,37 @@ __device__ __forceinline__ void process_bucket(const Rec16 *__restrict__ recs, u
         }
         items[slot] = it;
     }
-    __syncthreads();
+    bucket_sync<kGlobal>();
 }
 
-// Persistent LDS kernel: workgroups pull buckets from a queue.
+// Persistent LDS kernel: workgroup w processes buckets w, w + G, ...  The
+// loop counter, the bucket size and every branch around a barrier are
+// wave-uniform by construction (readfirstlane; no lane-0-only work in the
+// loop), so the compiler emits scalar control flow around each s_barrier --
+// tools/check_barrier_loops.py verifies this on the ISA at build time.  (A
+// work queue whose atomic was taken by lane 0 only let the compiler split the
+// loop by exec mask and desynchronise the barriers.)
 template <class Item>
 __global__ __launch_bounds__(kBoundThreads) void k_bound_lds(
     const Rec16 *recs, const int64_t *bstart, const uint32_t *bcnt, uint32_t B, uint32_t M,
-    uint32_t *queue, BoundParams bp, Item *items, uint32_t *item_cursor, uint32_t *oversize,
-    uint32_t *n_oversize) {
+    BoundParams bp, Item *items, uint32_t *item_cursor, uint8_t *oversize_flag) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    BucketShared &sh = *reinterpret_cast<BucketShared *>(
+    BucketShared *sh = reinterpret_cast<BucketShared *>(
         smem + BucketLayout::make(M, ItemTraits<Item>::var, 2).total);
-    while (true) {
-        if (threadIdx.x == 0) sh.bucket = atomicAdd(queue, 1u);
-        __syncthreads();
-        const uint32_t b = sh.bucket;
-        __syncthreads();
-        if (b >= B) break;
-        const uint32_t n = bcnt[b];
-        if (n == 0) continue;
+    for (uint32_t b = blockIdx.x; b < B; b += gridDim.x) {
+        const uint32_t n = __builtin_amdgcn_readfirstlane(bcnt[b]);
         if (n > M) {
-            if (threadIdx.x == 0) oversize[atomicAdd(n_oversize, 1u)] = b;
-            continue;
+            oversize_flag[b] = 1;  // written by every lane: no divergent branch
+        } else if (n > 0) {
+            process_bucket<Item, uint16_t>(recs + bstart[b], n, smem, sh, bp, items, item_cursor);
         }
-        process_bucket<Item, uint16_t>(recs + bstart[b], n, smem, &sh, bp, items, item_cursor);
     }
+}
+
+// list of flagged buckets (rare): one atomic per flagged bucket
+__global__ void k_collect_flags(const uint8_t *flag, uint32_t B, uint32_t *list, uint32_t *count) {
+    for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < B; b += gridDim.x * blockDim.x)
+        if (flag[b]) list[atomicAdd(count, 1u)] = b;
 }
 
 // Oversize buckets: one workgroup per bucket, working set in global memory.
@@ -467,8 +514,9 @@ __global__ __launch_bounds__(kBoundThreads) void k_bound_global(
     uint32_t *item_cursor) {
     __shared__ BucketShared sh;
     const uint32_t b = list[blockIdx.x];
-    process_bucket<Item, uint32_t>(recs + bstart[b], bcnt[b], scratch + scratch_off[blockIdx.x], &sh, bp,
+    process_bucket<Item, uint32_t>(recs + bstart[b], __builtin_amdgcn_readfirstlane(bcnt[b]), scratch + scratch_off[blockIdx.x], &sh, bp,
                          items, item_cursor);
+    mark(bp, 9);
 }
 
 }  // namespace dpg

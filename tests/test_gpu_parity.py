@@ -117,3 +117,63 @@ def test_gpu_selection_and_noise_match_oracle(built):
     got_ids = out.partition_ids.cpu().numpy()
     assert np.array_equal(np.sort(got_ids), ids)
     assert np.allclose(out.values.cpu().numpy(), o[ids], rtol=1e-12, atol=1e-6)
+
+
+@pytest.mark.parametrize("target,cap", [(1024, 2048), (16, 2048), (1024, 64), (8, 48)],
+                         ids=["default", "3levels", "global_path", "mixed"])
+def test_gpu_partition_levels_and_fallback(built, target, cap):
+    """Multi-level partitioning and the global-memory path for oversize
+    buckets give exactly the oracle's partials (tuning hook dpg_set_tuning)."""
+    P = 5000
+    pid, pk, val = _dataset(21, 250_000, 2_500, P, zipf=1.1)   # ~100 records / pid
+    params = pdp.AggregateParams(metrics=[pdp.Metrics.COUNT, pdp.Metrics.SUM,
+                                          pdp.Metrics.PRIVACY_ID_COUNT],
+                                 max_partitions_contributed=8, max_contributions_per_partition=2,
+                                 min_value=0.0, max_value=10.0)
+    backend = pdp.MI355XBackend(device=0, seed=SEED)
+    backend.ctx.set_tuning(target, cap)
+    acc = pdp.NaiveBudgetAccountant(1.0, 1e-6)
+    res = pdp.DPEngine(acc, backend).aggregate(
+        pdp.ColumnarData(pid=torch.as_tensor(pid), pk=torch.as_tensor(pk),
+                         value=torch.as_tensor(val), n_partitions=P),
+        params, pdp.DataExtractors("pid", "pk", "value"), public_partitions=list(range(P)))
+    acc.compute_budgets()
+    res.noise_enabled = False
+    res.materialize()
+    ref = oracle.bound_aggregate(pid, pk, val, res.plan.bound_fields(P), SEED,
+                                 public_mask=oracle.bitmap(range(P), P))
+    got = {k: v.cpu().numpy() for k, v in res.last_partials.items() if v is not None}
+    assert np.array_equal(got["rows"], ref["rows"])
+    assert np.array_equal(got["count"], ref["count"])
+    assert np.allclose(got["sum"], ref["sum"], rtol=1e-9, atol=1e-9)
+
+
+def test_gpu_empty_and_single_record(built):
+    params = pdp.AggregateParams(metrics=[pdp.Metrics.COUNT, pdp.Metrics.SUM],
+                                 max_partitions_contributed=1, max_contributions_per_partition=1,
+                                 min_value=0.0, max_value=1.0)
+    _, out = run_engine(np.array([7]), np.array([3]), np.array([0.5]), params, public=[3, 4])
+    keys = out.keys()
+    vals = out.values.cpu().numpy()
+    got = dict(zip(keys, vals.tolist()))
+    assert got == {3: [1.0, 0.5], 4: [0.0, 0.0]}
+
+
+def test_gpu_key_range_error(built):
+    params = pdp.AggregateParams(metrics=[pdp.Metrics.COUNT], max_partitions_contributed=1,
+                                 max_contributions_per_partition=1)
+    with pytest.raises(ValueError, match="out of range"):
+        run_engine(np.array([1, 2]), np.array([0, 10]), None, params, n_partitions=5)
+
+
+def test_gpu_determinism_same_seed(built):
+    P = 2000
+    pid, pk, val = _dataset(3, 200_000, 5_000, P)
+    params = pdp.AggregateParams(metrics=[pdp.Metrics.COUNT, pdp.Metrics.SUM,
+                                          pdp.Metrics.PRIVACY_ID_COUNT],
+                                 max_partitions_contributed=2, max_contributions_per_partition=1,
+                                 min_value=0.0, max_value=10.0)
+    a = run_engine(pid, pk, val, params, noise=True, n_partitions=P)[1]
+    b = run_engine(pid, pk, val, params, noise=True, n_partitions=P)[1]
+    assert np.array_equal(a.partition_ids.cpu().numpy(), b.partition_ids.cpu().numpy())
+    assert np.allclose(a.values.cpu().numpy(), b.values.cpu().numpy(), rtol=1e-12, atol=1e-9)

@@ -1,0 +1,106 @@
+"""Known answers of the un-vendored PyDP boundary, restated from the
+reference's own tests, for both the product's host math and the oracle."""
+import math
+
+import numpy as np
+import pytest
+
+import pipelinedp_amd as pdp
+from oracle import mechanisms as om
+from pipelinedp_amd import dp_computations as dpc
+from pipelinedp_amd import partition_selection as ps
+
+# tests/dp_computations_test.py:62-67, 371-405, 485-545 (reference)
+SIGMA_GOLDENS = [
+    (0.5, 1e-10, 10.0, 114.375),
+    (2.0, 1e-8, math.sqrt(2) * 10.0, 37.53742639189524),
+    (1.0, 1e-5, 5.0, 18.662109375),
+    (1.0, 1e-10, 15.0, 88.06640625),
+    (2.0, 1e-15, 4.5, 17.1826171875),
+    (0.1, 1e-5, 0.55, 16.9125),
+    (0.2, 1e-10, 10.0, 277.34375),
+]
+
+
+@pytest.mark.parametrize("eps,delta,l2,want", SIGMA_GOLDENS)
+def test_gaussian_sigma_goldens(eps, delta, l2, want):
+    assert dpc.compute_sigma(eps, delta, l2) == pytest.approx(want, rel=1e-12)
+    assert om.gaussian_sigma(eps, delta, l2) == pytest.approx(want, rel=1e-12)
+
+
+def test_gaussian_describe_golden():
+    # tests/dp_computations_test.py:485-490
+    m = dpc.AdditiveMechanism(pdp.NoiseKind.GAUSSIAN, 1.0, 1e-10, dpc.Sensitivities(l2=15))
+    assert m.describe() == ("Gaussian mechanism:  parameter=88.06640625  eps=1.0  "
+                            "delta=1e-10  l2_sensitivity=15")
+
+
+def test_laplace_parameter():
+    # tests/dp_computations_test.py:429-459: b = l1 / eps
+    m = dpc.AdditiveMechanism(pdp.NoiseKind.LAPLACE, 0.5, 0, dpc.Sensitivities(l0=4, linf=3))
+    assert m.noise_parameter == pytest.approx(24.0)
+
+
+def _pmf_binomial(n, p):
+    return [math.comb(n, k) * p**k * (1 - p)**(n - k) for k in range(n + 1)]
+
+
+@pytest.mark.parametrize("table_fn", [
+    lambda e, d, l0: ps.truncated_geometric_table(e, d, l0),
+    lambda e, d, l0: om.truncated_geometric_table(e, d, l0),
+], ids=["product", "oracle"])
+def test_truncated_geometric_goldens(table_fn):
+    # analysis/tests/per_partition_combiners_test.py:200-238 (reference)
+    t = table_fn(1.0, 1e-5, 1)
+    assert t[10] == pytest.approx(0.12818308050524607, abs=1e-10)
+    pmf = _pmf_binomial(100, 0.1)
+    prob = sum(p * (t[k] if k < len(t) else 1.0) for k, p in enumerate(pmf))
+    assert prob == pytest.approx(0.3321336253750503, abs=1e-10)
+    t = table_fn(100, 0.5, 1)  # "Large eps delta": 100 ids -> kept surely
+    assert (t[100] if len(t) > 100 else 1.0) == 1.0
+
+
+def test_pre_threshold_shift():
+    # n = 12 with pre_threshold = 3 behaves as n = 10 (same reference test)
+    plan = ps.create_partition_selection_strategy(
+        pdp.PartitionSelectionStrategy.TRUNCATED_GEOMETRIC, 1.0, 1e-5, 1, 3)
+    assert ps.probability_of_keep(plan, 12) == pytest.approx(0.12818308050524607, abs=1e-10)
+    assert ps.probability_of_keep(plan, 2) == 0.0
+
+
+@pytest.mark.parametrize("strategy", [pdp.PartitionSelectionStrategy.LAPLACE_THRESHOLDING,
+                                      pdp.PartitionSelectionStrategy.GAUSSIAN_THRESHOLDING])
+def test_threshold_strategies_are_dp_at_n1(strategy):
+    """Sanity (parity unpinned): a partition with one privacy id is kept with
+    probability <= delta' (l0-adjusted delta)."""
+    eps, delta, l0 = 1.0, 1e-5, 3
+    plan = ps.create_partition_selection_strategy(strategy, eps, delta, l0)
+    assert ps.probability_of_keep(plan, 1) <= ps.adjusted_delta(delta, l0) * 1.0001
+    assert ps.probability_of_keep(plan, 10_000) > 0.999
+    # product and oracle restatements agree
+    if strategy == pdp.PartitionSelectionStrategy.LAPLACE_THRESHOLDING:
+        thr, b = om.laplace_threshold(eps, delta, l0)
+    else:
+        thr, b = om.gaussian_threshold(eps, delta, l0)
+    assert plan.threshold == pytest.approx(thr, rel=1e-9)
+    assert plan.noise_scale == pytest.approx(b, rel=1e-12)
+
+
+def test_equally_split_budget():
+    # tests/dp_computations_test.py (test_equally_split_budget)
+    with pytest.raises(ValueError):
+        dpc.equally_split_budget(0.5, 1e-10, 0)
+    assert dpc.equally_split_budget(0.5, 1e-10, 1) == [(0.5, 1e-10)]
+    want = [(0.5 / 5, 1e-10 / 5)] * 4 + [(0.5 - 4 * (0.5 / 5), 1e-10 - 4 * (1e-10 / 5))]
+    got = dpc.equally_split_budget(0.5, 1e-10, 5)
+    assert np.allclose(got, want, rtol=0, atol=1e-18)
+
+
+def test_sensitivities():
+    assert dpc.compute_l2_sensitivity(4.5, 12.123) == pytest.approx(25.716766525, abs=0.1)
+    with pytest.raises(ValueError):
+        dpc.Sensitivities(l0=1)
+    with pytest.raises(ValueError):
+        dpc.Sensitivities(l0=1, linf=0)
+    s = dpc.Sensitivities(l0=4, linf=2)
+    assert (s.l1, s.l2) == (8, 4.0)
