@@ -1,0 +1,42 @@
+"""Ingest: dictionary encoding of partition keys / privacy ids (CPU tensors)."""
+import numpy as np
+import torch
+
+import pipelinedp_amd as pdp
+from pipelinedp_amd import columnar
+
+CPU = torch.device("cpu")
+EX = pdp.DataExtractors(lambda r: r[0], lambda r: r[1], lambda r: r[2])
+
+
+def test_dense_integer_keys_pass_through():
+    col = pdp.ColumnarData(pid=np.array([5, 6]), pk=np.array([3, 1]), value=np.array([1.0, 2.0]))
+    enc = columnar.encode(col, pdp.DataExtractors("pid", "pk", "value"), CPU, True)
+    assert enc.key_table is None and enc.n_partitions == 4
+    assert enc.pk.tolist() == [3, 1]
+
+
+def test_string_keys_are_encoded_and_decoded():
+    rows = [("u1", "b", 1.0), ("u2", "a", 2.0), ("u1", "c", 3.0)]
+    enc = columnar.encode(rows, EX, CPU, True, public_partitions=["a", "z"])
+    assert enc.n_partitions == 4
+    keys = columnar.decode_keys(np.arange(enc.n_partitions), enc.key_table)
+    assert sorted(keys) == ["a", "b", "c", "z"]
+    assert [keys[i] for i in enc.pk.tolist()] == ["b", "a", "c"]
+    assert enc.public_count == 2
+    assert enc.pid.max() < 2 and enc.pid.min() >= 0
+
+
+def test_large_and_negative_keys_are_encoded():
+    rows = [(-5, 10**12, 1.0), (2**40, 7, 2.0)]
+    enc = columnar.encode(rows, EX, CPU, True)
+    assert enc.key_table is not None and enc.n_partitions == 2
+    assert enc.pid.min() >= 0 and enc.pid.max() < 2**32 - 1
+
+
+def test_public_bitmap():
+    col = pdp.ColumnarData(pid=np.array([1]), pk=np.array([2]), value=np.array([0.0]))
+    enc = columnar.encode(col, pdp.DataExtractors("pid", "pk", "value"), CPU, True,
+                          public_partitions=[0, 2, 9])
+    bits = np.unpackbits(enc.public_mask.numpy(), bitorder="little")[:enc.n_partitions]
+    assert np.nonzero(bits)[0].tolist() == [0, 2, 9]
