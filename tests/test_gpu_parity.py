@@ -162,7 +162,7 @@ def test_gpu_empty_and_single_record(built):
 def test_gpu_key_range_error(built):
     params = pdp.AggregateParams(metrics=[pdp.Metrics.COUNT], max_partitions_contributed=1,
                                  max_contributions_per_partition=1)
-    with pytest.raises(ValueError, match="out of range"):
+    with pytest.raises(ValueError, match="outside"):
         run_engine(np.array([1, 2]), np.array([0, 10]), None, params, n_partitions=5)
 
 
