@@ -159,10 +159,12 @@ int dpg_last_error(dpg_ctx *ctx, char *buf, size_t len);
 int dpg_set_seed(dpg_ctx *ctx, uint64_t seed);
 
 /* Tuning / testing hook: average records per privacy-id bucket the
- * partition levels aim for (default 1024; smaller values force more levels
- * on small inputs) and the largest bucket processed in LDS (default and
- * maximum 2048; larger buckets take the global-memory path).  <= 0 keeps
- * the current value. */
+ * partition levels aim for (default: half the chunk capacity; smaller values
+ * force more levels on small inputs) and the chunk capacity, i.e. the most
+ * records bounded together in LDS (default and maximum 2048 for COUNT/SUM,
+ * 1536 with MEAN/VARIANCE).  Buckets over the capacity are split by further
+ * privacy-id hash bits; a bucket still over it takes the global-memory path.
+ * <= 0 keeps the current value. */
 int dpg_set_tuning(dpg_ctx *ctx, int32_t bucket_target, int32_t bucket_cap);
 
 /* Contribution bounding + per-(pid,pk) accumulators + merge per partition.

@@ -3,7 +3,9 @@
 //
 // Pipeline of dpg_bound_aggregate (DESIGN.md "Kernels"):
 //   partition levels (hist, scan, digit base, scatter) by privacy-id hash
-//   -> k_bound_lds (+ k_bound_global for oversize buckets)
+//   -> k_make_chunks (greedy packing of fine buckets), refine level for
+//      oversize buckets -> k_bound_chunks (+ k_bound_global for single
+//      buckets still over the chunk capacity)
 //   -> one partition-key-range level over the kept pairs -> k_reduce_items
 #include <hip/hip_runtime.h>
 
@@ -19,6 +21,7 @@
 #include <vector>
 
 #include "dpg_bound.h"
+#include "dpg_chunk.h"
 #include "dpg_common.h"
 #include "dpg_partition.h"
 #include "dpg_select.h"
@@ -27,8 +30,10 @@ using namespace dpg;
 
 namespace {
 
-constexpr uint32_t kBucketCap = 2048;      // records per bucket processed in LDS
-constexpr uint32_t kBucketTarget = 1024;   // average bucket size the levels aim for
+constexpr int kCap16 = 2048;   // chunk capacity (records) of the COUNT/SUM kernel
+constexpr int kCap32 = 1536;   // chunk capacity of the MEAN/VARIANCE kernel
+constexpr uint32_t kBucketCap = 2048;
+constexpr uint32_t kChunkGroup = 32;  // fine buckets per packing thread
 constexpr int kMaxLevels = 3;
 
 struct Buf {
@@ -40,12 +45,17 @@ struct Control {  // device-side counters, zeroed per call
     uint32_t err;
     uint32_t queue;
     uint32_t item_cursor;
-    uint32_t n_oversize;
+    uint32_t n_oversize;  // buckets left for the global-memory path
     uint32_t ntiles[8];
     int64_t nvalid;
     int64_t n_scalar;
     int64_t kept_total;
-    uint32_t pad[4];
+    uint32_t n_chunks;
+    uint32_t n_over;      // fine buckets over the chunk capacity
+    uint32_t n_over2;     // refined buckets still over it
+    uint32_t pad0;
+    unsigned long long over_records;
+    unsigned long long over2_records;
 };
 
 }  // namespace
@@ -60,7 +70,7 @@ struct dpg_ctx {
     std::vector<hipEvent_t> events;
     int n_events_used = 0;
     hipStream_t last_stream = nullptr;
-    uint32_t bucket_target = kBucketTarget;
+    uint32_t bucket_target = 0;  // 0: half the chunk capacity
     uint32_t bucket_cap = kBucketCap;
 };
 
@@ -158,7 +168,7 @@ template <class Src, class Rec, class Dig, int IPT>
 int run_level(dpg_ctx *ctx, hipStream_t s, Src src, Dig dig, uint32_t S, const int64_t *seg_start,
               const uint32_t *seg_cnt, const int64_t *seg_cnt64, int64_t n_upper, uint32_t F,
               uint32_t bits, Rec *out, const char *tag, int64_t **base_out, uint32_t **tot_out,
-              uint32_t *ntiles_dev) {
+              uint32_t *ntiles_dev, const int64_t *out_start = nullptr) {
     int st = DPG_OK;
     const int64_t sub = (int64_t)kPartThreads * IPT;
     int64_t tile = std::max<int64_t>(sub, ((n_upper / 3072 + sub - 1) / sub) * sub);
@@ -173,12 +183,13 @@ int run_level(dpg_ctx *ctx, hipStream_t s, Src src, Dig dig, uint32_t S, const i
     k_build_tiles<<<(S + 255) / 256, 256, 0, s>>>(seg_start, seg_cnt, seg_cnt64, S, tile, tiles, stb,
                                                   snt, ntiles_dev);
     LAUNCH_CHECK();
-    k_hist<Src, Rec, Dig><<<max_tiles, kPartThreads, 4 * F * sizeof(uint32_t), s>>>(
-        src, dig, tiles, ntiles_dev, F, hist);
+    auto hsrc = hist_view(src);
+    k_hist<decltype(hsrc), Rec, Dig><<<max_tiles, kPartThreads, 4 * F * sizeof(uint32_t), s>>>(
+        hsrc, dig, tiles, ntiles_dev, F, hist);
     LAUNCH_CHECK();
     k_scan_tiles<<<dim3(S, (F + 63) / 64), 1024, 0, s>>>(stb, snt, F, hist, tot);
     LAUNCH_CHECK();
-    k_digit_base<<<S, 1024, 0, s>>>(seg_start, F, tot, base, nullptr);
+    k_digit_base<<<S, 1024, 0, s>>>(out_start ? out_start : seg_start, F, tot, base, nullptr);
     LAUNCH_CHECK();
     size_t lds = sizeof(Rec) * sub + 1024 * 4 * 2 + 1024 * 8 + 16 * 4;
     k_scatter<Src, Rec, Dig, IPT><<<max_tiles, kPartThreads, lds, s>>>(src, dig, tiles, ntiles_dev,
@@ -209,60 +220,154 @@ BoundParams to_bound(const dpg_bound_params *p, uint64_t seed) {
 
 template <class Item>
 int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Rec16 *recs, const int64_t *bstart,
-                     const uint32_t *bcnt, uint32_t B, const BoundParams &bp, Item *items,
-                     Item *items2, int64_t n, int64_t P, const dpg_partials *out, Control *ctl) {
+                     const uint32_t *bcnt, uint32_t B, uint32_t hash_bits_left,
+                     const BoundParams &bp, Item *items, Item *items2, int64_t n, int64_t P,
+                     const dpg_partials *out, Control *ctl) {
     int st = DPG_OK;
-    WS(oversize, uint32_t, "bound.oversize", B);
-    WS(oflag, uint8_t, "bound.oflag", B);
-    HIP_TRY(hipMemsetAsync(oflag, 0, B, s));
-    const size_t lds = BucketLayout::make(kBucketCap, ItemTraits<Item>::var, 2).total +
-                       align16(sizeof(BucketShared));
-    stage(ctx, s, "bound");
-    BoundParams bpl = bp;
-    uint32_t *prog = watchdog_seconds() ? watchdog_buffer(ctx->n_cu) : nullptr;
-    bpl.progress = prog;
-    k_bound_lds<Item><<<ctx->n_cu, kBoundThreads, lds, s>>>(recs, bstart, bcnt, B, ctx->bucket_cap,
-                                                            bpl, items, &ctl->item_cursor, oflag);
+    constexpr int kCap = ItemTraits<Item>::var ? kCap32 : kCap16;
+    using CL = ChunkLayout<Item, kCap>;
+    const uint32_t cap = std::min<uint32_t>(ctx->bucket_cap, (uint32_t)kCap);
+    // ---- pack fine buckets into chunks
+    stage(ctx, s, "chunks");
+    WS(chunks, uint2, "chunks", B);
+    WS(ostart, int64_t, "over.start", B);
+    WS(ocnt, uint32_t, "over.cnt", B);
+    const uint32_t ngroups = (B + kChunkGroup - 1) / kChunkGroup;
+    k_make_chunks<<<(ngroups + 255) / 256, 256, 0, s>>>(bstart, bcnt, B, kChunkGroup, cap, 0u,
+                                                         chunks, &ctl->n_chunks, ostart, ocnt,
+                                                         &ctl->n_over, &ctl->over_records);
     LAUNCH_CHECK();
-    if (prog) watchdog_wait(s, prog, ctx->n_cu, "k_bound_lds");
-    k_collect_flags<<<std::min<uint32_t>((B + 255) / 256, 1024), 256, 0, s>>>(oflag, B, oversize,
-                                                                               &ctl->n_oversize);
-    LAUNCH_CHECK();
-    // oversize buckets (rare): global-memory working sets
     Control hctl;
     HIP_TRY(hipMemcpyAsync(&hctl, ctl, sizeof(Control), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     if (hctl.err & 1u)
         return fail(ctx, DPG_ERR_KEY_RANGE,
                     "privacy id outside [0, 2^32-1) or partition key outside [0, P)");
-    if (hctl.err & 2u) return fail(ctx, DPG_ERR_HIP, "internal hash-table error in bounding");
-    if (hctl.n_oversize > 0) {
-        const uint32_t no = hctl.n_oversize;
-        std::vector<uint32_t> list(no), cnt(B);
-        HIP_TRY(hipMemcpy(list.data(), oversize, no * 4, hipMemcpyDeviceToHost));
-        HIP_TRY(hipMemcpy(cnt.data(), bcnt, (size_t)B * 4, hipMemcpyDeviceToHost));
-        std::vector<size_t> off(no);
+    const uint2 *chunk_list = chunks;
+    const Rec16 *refined = recs;
+    // global-memory leftovers: (buffer, starts, counts, number)
+    const Rec16 *g_base = recs;
+    const int64_t *g_start = ostart;
+    const uint32_t *g_cnt = ocnt;
+    uint32_t n_global = 0;
+    if (hctl.n_over > 0) {
+        const uint32_t rbits = std::min<uint32_t>(10u, hash_bits_left);
+        if (rbits == 0) {
+            n_global = hctl.n_over;
+        } else {
+            // ---- refine oversize buckets by further privacy-id hash bits
+            stage(ctx, s, "refine");
+            const uint32_t no = hctl.n_over, F2 = 1u << rbits;
+            std::vector<uint32_t> hc(no);
+            HIP_TRY(hipMemcpy(hc.data(), ocnt, no * 4, hipMemcpyDeviceToHost));
+            std::vector<int64_t> hout(no);
+            int64_t acc = 0;
+            for (uint32_t i = 0; i < no; ++i) hout[i] = acc, acc += hc[i];
+            WS(oout, int64_t, "over.out", no);
+            HIP_TRY(hipMemcpyAsync(oout, hout.data(), no * 8, hipMemcpyHostToDevice, s));
+            WS(rbuf, Rec16, "refined", std::max<int64_t>(acc, 1));
+            int64_t *base2;
+            uint32_t *tot2;
+            DigPid dig{hash_bits_left - rbits, F2 - 1};
+            int r = run_level<SrcAoS<Rec16>, Rec16, DigPid, kItemsPerThread>(
+                ctx, s, SrcAoS<Rec16>{recs}, dig, no, ostart, ocnt, nullptr, acc, F2, rbits, rbuf,
+                "refine", &base2, &tot2, &ctl->ntiles[3], oout);
+            if (r) return r;
+            const uint32_t B2 = no * F2;
+            WS(chunks2, uint2, "chunks.r", (size_t)hctl.n_chunks + B2);
+            HIP_TRY(hipMemcpyAsync(chunks2, chunks, (size_t)hctl.n_chunks * sizeof(uint2),
+                                   hipMemcpyDeviceToDevice, s));
+            WS(o2start, int64_t, "over2.start", B2);
+            WS(o2cnt, uint32_t, "over2.cnt", B2);
+            const uint32_t ng2 = (B2 + F2 - 1) / F2;
+            k_make_chunks<<<(ng2 + 255) / 256, 256, 0, s>>>(base2, tot2, B2, F2, cap, 1u, chunks2,
+                                                           &ctl->n_chunks, o2start, o2cnt,
+                                                           &ctl->n_over2, &ctl->over2_records);
+            LAUNCH_CHECK();
+            HIP_TRY(hipMemcpyAsync(&hctl, ctl, sizeof(Control), hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipStreamSynchronize(s));
+            chunk_list = chunks2;
+            refined = rbuf;
+            g_base = rbuf;
+            g_start = o2start;
+            g_cnt = o2cnt;
+            n_global = hctl.n_over2;
+        }
+    }
+    // ---- bounding of every chunk in LDS; workgroup g writes its items to
+    // items[wg_off[g], ...), the global-memory path after all of them
+    const uint32_t G = (uint32_t)std::min(ctx->n_cu, 1022);
+    WS(wg_rec, uint32_t, "wg.rec", G + 1);
+    WS(wg_off, int64_t, "wg.off", G + 2);
+    WS(wg_cnt, uint32_t, "wg.cnt", G + 1);
+    WS(wg_pre, int64_t, "wg.pre", G + 2);
+    k_wg_records<<<G, 256, 0, s>>>(chunk_list, &ctl->n_chunks, G, wg_rec);
+    LAUNCH_CHECK();
+    k_scan_small<<<1, 1024, 0, s>>>(wg_rec, G, wg_off, nullptr);
+    LAUNCH_CHECK();
+    HIP_TRY(hipMemsetAsync(wg_cnt + G, 0, 4, s));
+    stage(ctx, s, "bound");
+    BoundParams bpl = bp;
+    uint32_t *prog = watchdog_seconds() ? watchdog_buffer(G) : nullptr;
+    bpl.progress = prog;
+    const bool timing = std::getenv("DPG_PHASE_TIMING") != nullptr;
+    bpl.phase_cyc = nullptr;
+    if (timing) {
+        WS(pc, unsigned long long, "bound.phase_cyc", 16);
+        HIP_TRY(hipMemsetAsync(pc, 0, 16 * 8, s));
+        bpl.phase_cyc = pc;
+    }
+    k_bound_chunks<Item, kCap><<<G, kChunkThreads, CL::TOTAL, s>>>(
+        recs, refined, chunk_list, &ctl->n_chunks, bpl, items, wg_off, wg_cnt);
+    LAUNCH_CHECK();
+    stage(ctx, s, "bound.tail");
+    if (prog) watchdog_wait(s, prog, G, "k_bound_chunks");
+    if (timing) {
+        unsigned long long h[16];
+        HIP_TRY(hipMemcpy(h, bpl.phase_cyc, sizeof(h), hipMemcpyDeviceToHost));
+        static const char *nm[9] = {"-", "-", "A1.insert", "A2.lists", "C1.alloc",
+                                    "C2C3.mpc", "D.mcpp", "E.acc", "F.emit"};
+        unsigned long long tot = 0;
+        for (int i = 2; i <= 8; ++i) tot += h[i];
+        std::fprintf(stderr, "[dpg phase] chunks=%u over=%u over2=%u per-WG Mcycles:",
+                     hctl.n_chunks, hctl.n_over, hctl.n_over2);
+        for (int i = 2; i <= 8; ++i)
+            std::fprintf(stderr, " %s=%.3f(%.0f%%)", nm[i], h[i] / 1e6 / ctx->n_cu,
+                         100.0 * h[i] / (tot ? tot : 1));
+        std::fprintf(stderr, "\n");
+    }
+    // ---- single buckets beyond the chunk capacity: global-memory working sets
+    if (n_global > 0) {
+        std::vector<uint32_t> cnt(n_global);
+        HIP_TRY(hipMemcpy(cnt.data(), g_cnt, n_global * 4, hipMemcpyDeviceToHost));
+        std::vector<size_t> off(n_global);
         size_t total = 0;
-        for (uint32_t i = 0; i < no; ++i) {
+        for (uint32_t i = 0; i < n_global; ++i) {
             off[i] = total;
-            total += align16(BucketLayout::make(cnt[list[i]], ItemTraits<Item>::var, 4).total);
+            total += align16(BucketLayout::make(cnt[i], ItemTraits<Item>::var, 4).total);
         }
         WS(scratch, char, "bound.scratch", total);
-        WS(doff, size_t, "bound.scratch_off", no);
-        HIP_TRY(hipMemcpyAsync(doff, off.data(), no * sizeof(size_t), hipMemcpyHostToDevice, s));
+        WS(doff, size_t, "bound.scratch_off", n_global);
+        HIP_TRY(hipMemcpyAsync(doff, off.data(), n_global * sizeof(size_t), hipMemcpyHostToDevice,
+                               s));
         BoundParams bpg = bp;
-        uint32_t *gprog = watchdog_seconds() ? watchdog_buffer(no) : nullptr;
+        uint32_t *gprog = watchdog_seconds() ? watchdog_buffer(n_global) : nullptr;
         bpg.progress = gprog;
+        bpg.phase_cyc = nullptr;
         if (watchdog_seconds())
-            std::fprintf(stderr, "[dpg] %u oversize buckets, scratch %zu bytes\n", no, total);
-        k_bound_global<Item><<<no, kBoundThreads, 0, s>>>(recs, bstart, bcnt, oversize, doff,
-                                                          scratch, bpg, items, &ctl->item_cursor);
+            std::fprintf(stderr, "[dpg] %u oversize buckets, scratch %zu bytes\n", n_global, total);
+        k_bound_global<Item><<<n_global, kBoundThreads, 0, s>>>(g_base, g_start, g_cnt, doff,
+                                                                scratch, bpg, items, wg_off + G,
+                                                                wg_cnt + G);
         LAUNCH_CHECK();
-        if (gprog) watchdog_wait(s, gprog, no, "k_bound_global");
-        HIP_TRY(hipMemcpyAsync(&hctl, ctl, sizeof(Control), hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
-        if (hctl.err & 2u) return fail(ctx, DPG_ERR_HIP, "internal hash-table error (global path)");
+        if (gprog) watchdog_wait(s, gprog, n_global, "k_bound_global");
     }
+    k_scan_small<<<1, 1024, 0, s>>>(wg_cnt, G + 1, wg_pre, &ctl->item_cursor);
+    LAUNCH_CHECK();
+    HIP_TRY(hipMemcpyAsync(&hctl, ctl, sizeof(Control), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (hctl.err & 2u) return fail(ctx, DPG_ERR_HIP, "internal hash-table error in bounding");
+    const SrcSeg<Item> item_src{items, wg_pre, wg_off, G + 1};
     // ---- merge kept pairs per partition
     stage(ctx, s, "reduce");
     Partials po{out->rows, out->count, out->sum, out->nsum, out->nsq};
@@ -272,8 +377,8 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Rec16 *recs, const int64
         uint32_t bits = std::max<uint32_t>(1, ceil_log2((double)F));
         int64_t *baseR;
         uint32_t *totR;
-        int r = run_level<SrcAoS<Item>, Item, DigPk<Item>, (sizeof(Item) == 16 ? 8 : 4)>(
-            ctx, s, SrcAoS<Item>{items}, DigPk<Item>{(uint32_t)kRangeBits}, 1u, nullptr,
+        int r = run_level<SrcSeg<Item>, Item, DigPk<Item>, (sizeof(Item) == 16 ? 8 : 4)>(
+            ctx, s, item_src, DigPk<Item>{(uint32_t)kRangeBits}, 1u, nullptr,
             &ctl->item_cursor, nullptr, n, F, bits, items2, "items", &baseR, &totR,
             &ctl->ntiles[4]);
         if (r) return r;
@@ -289,7 +394,8 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Rec16 *recs, const int64
         k_reduce_items<Item><<<max_tiles, 1024, lds_r, s>>>(items2, rt, &ctl->ntiles[5], P, po);
         LAUNCH_CHECK();
     } else {
-        k_reduce_items_direct<Item><<<ctx->n_cu * 8, 256, 0, s>>>(items, &ctl->item_cursor, po);
+        k_reduce_items_direct<Item, SrcSeg<Item>><<<ctx->n_cu * 8, 256, 0, s>>>(
+            item_src, &ctl->item_cursor, po);
         LAUNCH_CHECK();
     }
     stage(ctx, s, "end");
@@ -308,10 +414,10 @@ dpg_ctx *dpg_ctx_create(int device, uint64_t seed) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->n_cu = prop.multiProcessorCount;
     // the bound kernel needs ~150 KB of dynamic LDS
-    (void)hipFuncSetAttribute((const void *)k_bound_lds<Item16>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void *)k_bound_lds<Item32>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void *)k_bound_chunks<Item16, kCap16>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void *)k_bound_chunks<Item32, kCap32>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     return c;
 }
 
@@ -392,7 +498,10 @@ int dpg_bound_aggregate(dpg_ctx *ctx, const int64_t *pid, const int64_t *pk, con
     WS(recB, Rec16, "recB", n);
 
     // ---- level plan: total hash bits so buckets average ~kBucketTarget
-    uint32_t bits_total = std::max<uint32_t>(1, ceil_log2((double)n / ctx->bucket_target));
+    const uint32_t target = ctx->bucket_target
+                                ? ctx->bucket_target
+                                : std::min<uint32_t>(ctx->bucket_cap, var ? kCap32 : kCap16) / 2;
+    uint32_t bits_total = std::max<uint32_t>(1, ceil_log2((double)n / std::max<uint32_t>(1, target)));
     int levels = (int)((bits_total + 9) / 10);
     if (levels > kMaxLevels) levels = kMaxLevels, bits_total = 10 * kMaxLevels;
     uint32_t lbits[kMaxLevels] = {0, 0, 0};
@@ -430,16 +539,18 @@ int dpg_bound_aggregate(dpg_ctx *ctx, const int64_t *pid, const int64_t *pk, con
     BoundParams bp = to_bound(p, ctx->seed);
     bp.err = &ctl->err;
     bp.progress = nullptr;
+    bp.phase_cyc = nullptr;
     Rec16 *other = (cur == recA) ? recB : recA;
     if (!var) {
         Item16 *items = reinterpret_cast<Item16 *>(other);
         Item16 *items2 = reinterpret_cast<Item16 *>(cur);
-        return bound_and_reduce<Item16>(ctx, s, cur, bstart, bcnt, B, bp, items, items2, n, P, out,
+        return bound_and_reduce<Item16>(ctx, s, cur, bstart, bcnt, B, shift, bp, items, items2, n, P, out,
                                          ctl);
     }
     WS(it32a, Item32, "items32a", n);
     WS(it32b, Item32, "items32b", n);
-    return bound_and_reduce<Item32>(ctx, s, cur, bstart, bcnt, B, bp, it32a, it32b, n, P, out, ctl);
+    return bound_and_reduce<Item32>(ctx, s, cur, bstart, bcnt, B, shift, bp, it32a, it32b, n, P, out,
+                                     ctl);
 }
 
 int dpg_select_and_noise(dpg_ctx *ctx, const dpg_partials *in, const dpg_select_params *sel,

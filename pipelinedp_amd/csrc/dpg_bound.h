@@ -2,7 +2,7 @@
 //
 // A bucket holds every record of a set of privacy ids (the top hash bits of
 // fmix32(pid) are the bucket id).  One 1024-thread workgroup processes a
-// bucket entirely in LDS:
+// bucket in a working set given by `base` (global scratch here):
 //   A1  insert every record's pid and (pid, pk) into LDS hash tables
 //   A2  dense ids for the occupied slots (block compaction)
 //   A3  per-pair record counts + record lists, per-pid pair counts
@@ -13,8 +13,9 @@
 //       PER_PRIVACY_ID mode, the L records per pid (:123-124)
 //   E   clipped per-pair accumulators            (combiners.py:255-500)
 //   F   emit one Item per kept pair (pk, count, sum[, nsum, nsq])
-// Buckets larger than the LDS capacity run the same code on a global-memory
-// scratch (k_bound_global).  "k smallest" uses an atomicMin cascade over k
+// This is the global-memory path for single buckets larger than the LDS chunk
+// capacity (k_bound_global); the LDS path is process_chunk (dpg_chunk.h),
+// which gives identical results.  "k smallest" uses an atomicMin cascade over k
 // slots per group; keys are distinct, so exactly k survive.
 #pragma once
 
@@ -39,12 +40,35 @@ struct BoundParams {
     uint64_t seed;
     uint32_t *err;       // bit 1: internal table error
     uint32_t *progress;  // debug watchdog: last phase per workgroup (or null)
+    unsigned long long *phase_cyc;  // debug: shader cycles per phase (or null)
 };
 
-__device__ __forceinline__ void mark(const BoundParams &bp, uint32_t phase) {
+// Debug hooks at phase boundaries: watchdog progress, and (DPG_PHASE_TIMING)
+// the shader cycles thread 0 spent since the previous mark, added to the
+// register accumulator pt[phase] (slot k = the phase that ends at mark k);
+// the kernel flushes pt once at exit, so timing adds no memory traffic to
+// the phases it measures.
+struct PhaseTimer {
+    uint64_t last;
+    uint64_t pt[10];
+};
+__device__ __forceinline__ void mark(const BoundParams &bp, uint32_t phase, PhaseTimer &tm) {
     if (bp.progress && threadIdx.x == 0)
         __hip_atomic_store(&bp.progress[blockIdx.x], phase, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
+    if (bp.phase_cyc) {
+        const uint64_t now = __builtin_amdgcn_s_memtime();
+        tm.pt[phase] += now - tm.last;
+        tm.last = now;
+    }
+}
+__device__ __forceinline__ void timer_start(const BoundParams &bp, PhaseTimer &tm) {
+    tm.last = bp.phase_cyc ? __builtin_amdgcn_s_memtime() : 0;
+    for (int k = 0; k < 10; ++k) tm.pt[k] = 0;
+}
+__device__ __forceinline__ void timer_flush(const BoundParams &bp, const PhaseTimer &tm) {
+    if (bp.phase_cyc && threadIdx.x == 0)
+        for (int k = 0; k < 10; ++k) atomicAdd(&bp.phase_cyc[k], (unsigned long long)tm.pt[k]);
 }
 
 __host__ __device__ __forceinline__ uint32_t next_pow2(uint32_t x) {
@@ -193,7 +217,7 @@ template <class Item, class Idx>
 __device__ __forceinline__ void process_bucket(const Rec16 *__restrict__ recs, uint32_t n,
                                                char *base, BucketShared *sh,
                                                const BoundParams &bp, Item *items,
-                                               uint32_t *item_cursor) {
+                                               uint32_t *item_cursor, PhaseTimer &clk) {
     constexpr bool kVar = ItemTraits<Item>::var;
     constexpr bool kGlobal = sizeof(Idx) == 4;
     uint32_t *err = bp.err;
@@ -238,7 +262,7 @@ __device__ __forceinline__ void process_bucket(const Rec16 *__restrict__ recs, u
     }
     if (tid == 0) sh->bump = 0;
     bucket_sync<kGlobal>();
-    mark(bp, 1);
+    mark(bp, 1, clk);
     // ---- A1: hash inserts
     for (uint32_t i = tid; i < n; i += kBoundThreads) {
         Rec16 r = recs[i];
@@ -246,7 +270,7 @@ __device__ __forceinline__ void process_bucket(const Rec16 *__restrict__ recs, u
         rec_pair[i] = (Idx)insert64(pairkey, cmask, ((uint64_t)r.pid << 32) | r.pk, err);
     }
     bucket_sync<kGlobal>();
-    mark(bp, 2);
+    mark(bp, 2, clk);
     // ---- A2: dense ids
     const uint32_t npid = block_enumerate<kGlobal>(C, pidkey, nullptr, pid_s2i, sh->sh16, &sh->npid);
     const uint32_t npair = block_enumerate<kGlobal>(C, nullptr, pairkey, pair_s2i, sh->sh16, &sh->npair);
@@ -261,7 +285,7 @@ __device__ __forceinline__ void process_bucket(const Rec16 *__restrict__ recs, u
         }
     }
     bucket_sync<kGlobal>();
-    mark(bp, 3);
+    mark(bp, 3, clk);
     // ---- A3: counts and lists
     const bool per_pid = bp.mode == DPG_MODE_PER_PRIVACY_ID;
     for (uint32_t i = tid; i < n; i += kBoundThreads) {
@@ -280,7 +304,7 @@ __device__ __forceinline__ void process_bucket(const Rec16 *__restrict__ recs, u
         for (uint32_t i = tid; i < n; i += kBoundThreads) vstage[i] = recs[i].v;
 
     if (!per_pid) {
-        mark(bp, 4);
+        mark(bp, 4, clk);
         // ---- C: cross-partition (mpc) selection over pairs
         for (uint32_t q = tid; q < npid; q += kBoundThreads) {
             uint32_t s = kNil;
@@ -313,7 +337,7 @@ __device__ __forceinline__ void process_bucket(const Rec16 *__restrict__ recs, u
         bucket_sync<kGlobal>();
         if (tid == 0) sh->bump = 0;
         bucket_sync<kGlobal>();
-        mark(bp, 5);
+        mark(bp, 5, clk);
         // ---- D: per-partition (mcpp) sampling inside kept pairs
         const bool sample = bp.mode == DPG_MODE_CROSS_AND_PER_PARTITION && bp.need_values;
         if (sample) {
@@ -394,7 +418,7 @@ __device__ __forceinline__ void process_bucket(const Rec16 *__restrict__ recs, u
         bucket_sync<kGlobal>();
     }
 
-    mark(bp, 6);
+    mark(bp, 6, clk);
     // ---- E: accumulators of kept records (slots/rkey dead; acc overlays)
     const bool part_clip = bp.sum_mode == DPG_SUM_CLIP_PARTITION;
     if (bp.need_values) {
@@ -424,7 +448,7 @@ __device__ __forceinline__ void process_bucket(const Rec16 *__restrict__ recs, u
         }
         bucket_sync<kGlobal>();
     }
-    mark(bp, 7);
+    mark(bp, 7, clk);
     // ---- F: emit kept pairs
     uint32_t kept_here = 0;
     for (uint32_t p = tid; p < npair; p += kBoundThreads) {
@@ -474,49 +498,25 @@ __device__ __forceinline__ void process_bucket(const Rec16 *__restrict__ recs, u
         items[slot] = it;
     }
     bucket_sync<kGlobal>();
+    mark(bp, 8, clk);
 }
 
-// Persistent LDS kernel: workgroup w processes buckets w, w + G, ...  The
-// loop counter, the bucket size and every branch around a barrier are
-// wave-uniform by construction (readfirstlane; no lane-0-only work in the
-// loop), so the compiler emits scalar control flow around each s_barrier --
-// tools/check_barrier_loops.py verifies this on the ISA at build time.  (A
-// work queue whose atomic was taken by lane 0 only let the compiler split the
-// loop by exec mask and desynchronise the barriers.)
-template <class Item>
-__global__ __launch_bounds__(kBoundThreads) void k_bound_lds(
-    const Rec16 *recs, const int64_t *bstart, const uint32_t *bcnt, uint32_t B, uint32_t M,
-    BoundParams bp, Item *items, uint32_t *item_cursor, uint8_t *oversize_flag) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    BucketShared *sh = reinterpret_cast<BucketShared *>(
-        smem + BucketLayout::make(M, ItemTraits<Item>::var, 2).total);
-    for (uint32_t b = blockIdx.x; b < B; b += gridDim.x) {
-        const uint32_t n = __builtin_amdgcn_readfirstlane(bcnt[b]);
-        if (n > M) {
-            oversize_flag[b] = 1;  // written by every lane: no divergent branch
-        } else if (n > 0) {
-            process_bucket<Item, uint16_t>(recs + bstart[b], n, smem, sh, bp, items, item_cursor);
-        }
-    }
-}
-
-// list of flagged buckets (rare): one atomic per flagged bucket
-__global__ void k_collect_flags(const uint8_t *flag, uint32_t B, uint32_t *list, uint32_t *count) {
-    for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < B; b += gridDim.x * blockDim.x)
-        if (flag[b]) list[atomicAdd(count, 1u)] = b;
-}
-
-// Oversize buckets: one workgroup per bucket, working set in global memory.
+// Buckets beyond the LDS chunk capacity (a privacy id with thousands of
+// records): one workgroup per bucket, working set in global memory.
 template <class Item>
 __global__ __launch_bounds__(kBoundThreads) void k_bound_global(
-    const Rec16 *recs, const int64_t *bstart, const uint32_t *bcnt, const uint32_t *list,
-    const size_t *scratch_off, char *scratch, BoundParams bp, Item *items,
-    uint32_t *item_cursor) {
+    const Rec16 *recs, const int64_t *bstart, const uint32_t *bcnt, const size_t *scratch_off,
+    char *scratch, BoundParams bp, Item *items, const int64_t *item_off, uint32_t *item_cursor) {
     __shared__ BucketShared sh;
-    const uint32_t b = list[blockIdx.x];
-    process_bucket<Item, uint32_t>(recs + bstart[b], __builtin_amdgcn_readfirstlane(bcnt[b]), scratch + scratch_off[blockIdx.x], &sh, bp,
-                         items, item_cursor);
-    mark(bp, 9);
+    const uint32_t b = blockIdx.x;
+    PhaseTimer clk;
+    BoundParams bq = bp;
+    bq.phase_cyc = nullptr;
+    timer_start(bq, clk);
+    process_bucket<Item, uint32_t>(recs + bstart[b], __builtin_amdgcn_readfirstlane(bcnt[b]),
+                                   scratch + scratch_off[blockIdx.x], &sh, bq, items + *item_off,
+                                   item_cursor, clk);
+    mark(bq, 9, clk);
 }
 
 }  // namespace dpg

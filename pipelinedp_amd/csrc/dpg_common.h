@@ -39,10 +39,11 @@ __host__ __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k
                                                        uint32_t k1) {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
-        uint32_t lo0 = 0xD2511F53u * c[0];
-        uint32_t hi0 = __umulhi(0xD2511F53u, c[0]);
-        uint32_t lo1 = 0xCD9E8D57u * c[2];
-        uint32_t hi1 = __umulhi(0xCD9E8D57u, c[2]);
+        // full 32x32->64 products: one v_mad_u64_u32 each on gfx950
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+        const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
+        const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
         uint32_t n0 = hi1 ^ c[1] ^ k0;
         uint32_t n2 = hi0 ^ c[3] ^ k1;
         c[0] = n0;

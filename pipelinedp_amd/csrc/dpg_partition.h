@@ -27,9 +27,12 @@ struct TileDesc {
 
 // ---------------------------------------------------------------- sources
 // Level 1: the caller's structure-of-arrays input (int64 pid, int64 pk,
-// double value) -> Rec16.  Drops records of non-public partitions and flags
-// keys outside the supported range.
+// double value) -> Rec16.  Drops records of non-public partitions.  Keys
+// outside the supported range raise err bit 1 (the call then fails); such a
+// record is still kept, so the scatter agrees with the histogram, which only
+// reads pid (and pk when there is a public-partition filter).
 struct SrcSoA {
+    static constexpr bool kPlainFetch = false;
     const int64_t *pid;
     const int64_t *pk;
     const double *v;
@@ -37,24 +40,76 @@ struct SrcSoA {
     int64_t P;
     uint32_t *err;
     __device__ __forceinline__ bool load(int64_t i, Rec16 &r) const {
-        int64_t a = pid[i], b = pk[i];
+        const int64_t a = pid[i], b = pk[i];
         r.v = v ? v[i] : 0.0;
-        if ((uint64_t)a >= 0xFFFFFFFFull || (uint64_t)b >= (uint64_t)P) {
-            atomicOr(err, 1u);
-            return false;
-        }
         r.pid = (uint32_t)a;
         r.pk = (uint32_t)b;
-        if (pub && !((pub[b >> 3] >> (b & 7)) & 1)) return false;
+        const bool in_range = (uint64_t)a < 0xFFFFFFFFull && (uint64_t)b < (uint64_t)P;
+        if (!in_range) atomicOr(err, 1u);
+        return !(pub && in_range && !((pub[b >> 3] >> (b & 7)) & 1));
+    }
+};
+
+// The level-1 histogram's view of SrcSoA: the same keep decision, reading
+// only what it needs.
+struct SrcSoAHist {
+    const int64_t *pid;
+    const int64_t *pk;
+    const uint8_t *pub;
+    int64_t P;
+    __device__ __forceinline__ bool load(int64_t i, Rec16 &r) const {
+        const int64_t a = pid[i];
+        r.pid = (uint32_t)a;
+        if (!pub) return true;
+        const int64_t b = pk[i];
+        const bool in_range = (uint64_t)a < 0xFFFFFFFFull && (uint64_t)b < (uint64_t)P;
+        return !(in_range && !((pub[b >> 3] >> (b & 7)) & 1));
+    }
+};
+
+template <class Src>
+__host__ __device__ inline Src hist_view(const Src &s) {
+    return s;
+}
+__host__ __device__ inline SrcSoAHist hist_view(const SrcSoA &s) {
+    return SrcSoAHist{s.pid, s.pk, s.pub, s.P};
+}
+
+template <class T>
+struct SrcAoS {
+    static constexpr bool kPlainFetch = true;
+    const T *a;
+    __device__ __forceinline__ bool load(int64_t i, T &r) const {
+        r = a[i];
         return true;
     }
 };
 
+// Items of S per-workgroup regions read as one sequence: element i lives in
+// region s with pre[s] <= i < pre[s + 1], at a[off[s] + i - pre[s]].  Each
+// thread walks increasing i, so the region found last is cached in
+// registers and the binary search runs only when i leaves it.
 template <class T>
-struct SrcAoS {
+struct SrcSeg {
+    static constexpr bool kPlainFetch = false;
     const T *a;
-    __device__ __forceinline__ bool load(int64_t i, T &r) const {
-        r = a[i];
+    const int64_t *pre;  // [S + 1]
+    const int64_t *off;  // [S]
+    uint32_t S;
+    int64_t lo = 0, hi = 0, base = 0;  // cached region [lo, hi), a index = base + i
+    __device__ __forceinline__ bool load(int64_t i, T &r) {
+        if (i < lo || i >= hi) {
+            uint32_t l = 0, h = S;
+            while (h - l > 1) {
+                const uint32_t mid = (l + h) >> 1;
+                if (pre[mid] <= i) l = mid;
+                else h = mid;
+            }
+            lo = pre[l];
+            hi = pre[l + 1];
+            base = off[l] - lo;
+        }
+        r = a[base + i];
         return true;
     }
 };
@@ -99,7 +154,7 @@ __global__ void k_build_tiles(const int64_t *seg_start, const uint32_t *seg_cnt,
 
 // ---------------------------------------------------------------- hist
 template <class Src, class Rec, class Dig>
-__global__ __launch_bounds__(kPartThreads) void k_hist(Src src, Dig dig, const TileDesc *tiles,
+__global__ __launch_bounds__(kPartThreads) void k_hist(Src src_in, Dig dig, const TileDesc *tiles,
                                                        const uint32_t *ntiles, uint32_t F,
                                                        uint32_t *hist) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lh[];  // [4][F]
@@ -111,6 +166,7 @@ __global__ __launch_bounds__(kPartThreads) void k_hist(Src src, Dig dig, const T
     for (uint32_t d = tid; d < 4 * F; d += kPartThreads) lh[d] = 0;
     __syncthreads();
     uint32_t *my = lh + copy * F;
+    Src src = src_in;  // per-thread copy (sources may cache lookup state)
     int64_t i = td.begin + tid;
     for (; i + 3 * kPartThreads < td.end; i += 4 * kPartThreads) {
         Rec r[4];
@@ -241,7 +297,7 @@ __device__ __forceinline__ Rec from_words(const Words<Rec> &x) {
 }
 
 template <class Src, class Rec, class Dig, int IPT>
-__global__ __launch_bounds__(kPartThreads) void k_scatter(Src src, Dig dig, const TileDesc *tiles,
+__global__ __launch_bounds__(kPartThreads) void k_scatter(Src src_in, Dig dig, const TileDesc *tiles,
                                                           const uint32_t *ntiles, uint32_t F,
                                                           uint32_t bits, const uint32_t *off,
                                                           const int64_t *base, Rec *out) {
@@ -259,11 +315,61 @@ __global__ __launch_bounds__(kPartThreads) void k_scatter(Src src, Dig dig, cons
     if (t >= *ntiles) return;
     const TileDesc td = tiles[t];
     const int tid = threadIdx.x;
+    Src src = src_in;  // per-thread copy (sources may cache lookup state)
     for (uint32_t d = tid; d < F; d += kPartThreads) {
         cur[d] = base[(size_t)td.seg * F + d] + off[(size_t)t * F + d];
         cnt[d] = 0;
     }
     __syncthreads();
+    if constexpr (Src::kPlainFetch) {
+        // Software pipeline: the records of sub-tile j + 1 are fetched into
+        // the (then dead) registers right after sub-tile j is staged in LDS,
+        // so the loads are in flight during j's write-out.
+        Words<Rec> r[IPT];
+        bool inb[IPT];
+#pragma unroll
+        for (int j = 0; j < IPT; ++j) {
+            const int64_t i = td.begin + (int64_t)j * kPartThreads + tid;
+            inb[j] = i < td.end;
+            if (inb[j]) r[j] = to_words(src.a[i]);
+        }
+        for (int64_t sb = td.begin; sb < td.end; sb += sub) {
+            uint32_t dg[IPT], rk[IPT];
+#pragma unroll
+            for (int j = 0; j < IPT; ++j) dg[j] = inb[j] ? dig(from_words<Rec>(r[j])) : 0u;
+#pragma unroll
+            for (int j = 0; j < IPT; ++j) rk[j] = wave_agg_rank(cnt, dg[j], inb[j], bits);
+            __syncthreads();
+            uint32_t c = tid < (int)F ? cnt[tid] : 0u;
+            uint32_t total;
+            uint32_t e = block_excl_scan_1024(c, sh16, total);
+            if (tid < (int)F) dstart[tid] = e;
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < IPT; ++j)
+                if (inb[j]) stage[dstart[dg[j]] + rk[j]] = r[j];
+            __syncthreads();
+            const int64_t nb = sb + sub;
+#pragma unroll
+            for (int j = 0; j < IPT; ++j) {
+                const int64_t i = nb + (int64_t)j * kPartThreads + tid;
+                inb[j] = i < td.end;
+                if (inb[j]) r[j] = to_words(src.a[i]);
+            }
+            for (uint32_t k = tid; k < total; k += kPartThreads) {
+                Words<Rec> x = stage[k];
+                uint32_t dd = dig(from_words<Rec>(x));
+                *reinterpret_cast<Words<Rec> *>(&out[cur[dd] + (int64_t)(k - dstart[dd])]) = x;
+            }
+            __syncthreads();
+            if (tid < (int)F) {
+                cur[tid] += cnt[tid];
+                cnt[tid] = 0;
+            }
+            __syncthreads();
+        }
+        return;
+    }
     for (int64_t sb = td.begin; sb < td.end; sb += sub) {
         Words<Rec> r[IPT];
         uint32_t dg[IPT];

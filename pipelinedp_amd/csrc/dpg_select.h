@@ -74,12 +74,14 @@ __global__ __launch_bounds__(1024) void k_reduce_items(const Item *items, const 
 }
 
 // Fallback merge for very large partition spaces: one global atomic per item.
-template <class Item>
-__global__ void k_reduce_items_direct(const Item *items, const uint32_t *n_items, Partials out) {
+template <class Item, class Src>
+__global__ void k_reduce_items_direct(Src items, const uint32_t *n_items, Partials out) {
     constexpr bool kVar = ItemTraits<Item>::var;
     const uint32_t n = *n_items;
+    Src src = items;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        Item it = items[i];
+        Item it;
+        src.load(i, it);
         atomicAdd((unsigned long long *)&out.rows[it.pk], 1ull);
         atomicAdd((unsigned long long *)&out.count[it.pk], (unsigned long long)it.cnt);
         if (out.sum) atomicAdd(&out.sum[it.pk], it.sum);

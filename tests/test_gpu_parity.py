@@ -177,3 +177,64 @@ def test_gpu_determinism_same_seed(built):
     b = run_engine(pid, pk, val, params, noise=True, n_partitions=P)[1]
     assert np.array_equal(a.partition_ids.cpu().numpy(), b.partition_ids.cpu().numpy())
     assert np.allclose(a.values.cpu().numpy(), b.values.cpu().numpy(), rtol=1e-12, atol=1e-9)
+
+
+_NO_NOISE = dict(noise_kind=0, family=0, slot_mask=0, n_outputs=0, out_src=[0] * 8,
+                 scale=[0.0] * 4, mid=0.0, mean_const=0, msq_const=0,
+                 mean_const_value=0.0, msq_const_value=0.0)
+
+
+@pytest.mark.parametrize("strategy", [pdp.PartitionSelectionStrategy.TRUNCATED_GEOMETRIC,
+                                      pdp.PartitionSelectionStrategy.LAPLACE_THRESHOLDING,
+                                      pdp.PartitionSelectionStrategy.GAUSSIAN_THRESHOLDING],
+                         ids=["tg", "laplace", "gaussian"])
+def test_gpu_select_partitions_matches_oracle(built, strategy):
+    """DPEngine.select_partitions (dp_engine.py:201-278): cross-partition
+    bounding of distinct partitions per privacy id, then private selection;
+    the kept set equals the oracle's for the same seed."""
+    P = 20_000
+    pid, pk, _ = _dataset(21, 300_000, 40_000, P, zipf=1.1)
+    backend = pdp.MI355XBackend(device=0, seed=SEED)
+    acc = pdp.NaiveBudgetAccountant(1.0, 1e-5)
+    eng = pdp.DPEngine(acc, backend)
+    params = pdp.SelectPartitionsParams(max_partitions_contributed=3,
+                                        partition_selection_strategy=strategy)
+    cols = pdp.ColumnarData(pid=torch.as_tensor(pid), pk=torch.as_tensor(pk), n_partitions=P)
+    res = eng.select_partitions(cols, params, pdp.DataExtractors("pid", "pk"))
+    acc.compute_budgets()
+    out = res.materialize()
+    ref = oracle.bound_aggregate(pid, pk, None, res._bound_fields(P), SEED)
+    got_rows = res.last_partials["rows"].cpu().numpy()
+    assert np.array_equal(got_rows, ref["rows"])
+    keep, _ = oracle.select_and_noise(ref, res._select_fields(0, None), _NO_NOISE, SEED,
+                                      keep_table=getattr(res, "_table", None))
+    want = np.nonzero(keep)[0]
+    assert 0 < len(want) < P
+    assert np.array_equal(np.sort(out.partition_ids.cpu().numpy()), want)
+    assert sorted(res) == want.tolist()
+
+
+def test_gpu_heavy_privacy_ids(built):
+    """A few privacy ids with thousands of records: their buckets overflow the
+    LDS chunk capacity, are refined by further hash bits, and the heaviest go
+    to the global-memory path; results stay identical to the oracle."""
+    rng = np.random.default_rng(77)
+    P = 5_000
+    light_pid = rng.integers(0, 200_000, 1_500_000)
+    heavy = np.repeat(np.arange(10**6, 10**6 + 12), [3000, 2500, 2200, 5000, 9000, 2100,
+                                                     1500, 1200, 4000, 2049, 2047, 7000])
+    pid = np.concatenate([light_pid, heavy]).astype(np.int64)
+    rng.shuffle(pid)
+    pk = ((rng.zipf(1.2, len(pid)) - 1) % P).astype(np.int64)
+    val = rng.uniform(-1.0, 11.0, len(pid))
+    params = pdp.AggregateParams(
+        metrics=[pdp.Metrics.COUNT, pdp.Metrics.SUM, pdp.Metrics.PRIVACY_ID_COUNT],
+        max_partitions_contributed=40, max_contributions_per_partition=3,
+        min_value=0.0, max_value=10.0)
+    res, _ = run_engine(pid, pk, val, params, public=list(range(P)), n_partitions=P)
+    ref = oracle.bound_aggregate(pid, pk, val, res.plan.bound_fields(P), SEED,
+                                 public_mask=oracle.bitmap(range(P), P))
+    got = {k: v.cpu().numpy() for k, v in res.last_partials.items() if v is not None}
+    assert np.array_equal(got["rows"], ref["rows"])
+    assert np.array_equal(got["count"], ref["count"])
+    assert np.allclose(got["sum"], ref["sum"], rtol=1e-9, atol=1e-9)
