@@ -35,14 +35,14 @@ extern "C" {
 /* ---- status codes ---- */
 #define DPG_OK 0
 #define DPG_ERR_INVALID_ARG 1
-#define DPG_ERR_KEY_RANGE 2   /* pid outside [0, 2^32) or pk outside [0, P) */
+#define DPG_ERR_KEY_RANGE 2   /* pid outside its declared range or pk outside [0, P) */
 #define DPG_ERR_HIP 3
 #define DPG_ERR_OOM 4
 #define DPG_ERR_UNSUPPORTED 5
 
 /* ---- Philox key tags: domain separation of the keyed random streams ---- */
 #define DPG_TAG_PAIR 0x50414952u   /* pair priority      (pid, pk)              */
-#define DPG_TAG_REC 0x52454344u    /* record priority    (pid, pk, value, occ)  */
+#define DPG_TAG_REC 0x52454344u    /* record priority    (pid, pk, record id)   */
 #define DPG_TAG_SELECT 0x53454C45u /* partition selection (pk)                  */
 #define DPG_TAG_NOISE 0x4E4F4953u  /* metric noise        (pk, slot)            */
 
@@ -105,6 +105,14 @@ typedef struct dpg_bound_params {
     const uint8_t *public_mask;  /* bitmap of P bits (device memory for
                                     libdpg, host memory for the oracle);
                                     NULL = private partition selection */
+    int64_t pid_min;             /* privacy ids lie in [pid_min,        */
+    int64_t pid_count;           /*   pid_min + pid_count); pid_count <= 2^32.
+                                    0 = unknown: libdpg reduces min/max on
+                                    the device first                     */
+    int64_t rec_id_offset;       /* global id of input record 0: the
+                                    record sampler is keyed by
+                                    (pid, pk, rec_id_offset + i), so shards
+                                    of one dataset sample as the whole   */
 } dpg_bound_params;
 
 /* Dense per-partition partial accumulators (structure of arrays).

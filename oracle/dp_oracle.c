@@ -57,18 +57,19 @@ void dpo_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
     memcpy(out, c, sizeof(c));
 }
 
-static inline uint32_t pair_prio(uint64_t seed, uint32_t pid, uint32_t pk) {
+/* pair priority: philox(seed ^ TAG_PAIR; pid, pk) */
+static inline uint32_t pair_prio(uint64_t seed, uint64_t pid, uint32_t pk) {
     uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32) ^ DPG_TAG_PAIR};
-    uint32_t c[4] = {pid, pk, 0u, 0u};
+    uint32_t c[4] = {(uint32_t)pid, pk, (uint32_t)(pid >> 32), 0u};
     philox4x32_10(c, key);
     return c[0];
 }
 
-static inline uint64_t rec_prio(uint64_t seed, uint32_t pid, uint32_t pk,
-                                uint64_t vbits, uint32_t occ) {
-    uint32_t key[2] = {(uint32_t)seed ^ (occ * 0x9E3779B9u),
+/* record priority: philox(seed ^ TAG_REC; pid, pk, global record id) */
+static inline uint64_t rec_prio(uint64_t seed, uint64_t pid, uint32_t pk, uint64_t gidx) {
+    uint32_t key[2] = {(uint32_t)seed ^ ((uint32_t)(pid >> 32) * 0x9E3779B9u),
                        (uint32_t)(seed >> 32) ^ DPG_TAG_REC};
-    uint32_t c[4] = {pid, pk, (uint32_t)vbits, (uint32_t)(vbits >> 32)};
+    uint32_t c[4] = {(uint32_t)pid, pk, (uint32_t)gidx, (uint32_t)(gidx >> 32)};
     philox4x32_10(c, key);
     return ((uint64_t)c[0] << 32) | c[1];
 }
@@ -132,24 +133,22 @@ static double add_noise(int kind, double x, double scale, uint64_t seed,
 typedef struct {
     const int64_t *pid, *pk;
     const double *v;
+    const int64_t *rec_ids; /* global record ids (NULL: rec_id_offset + i) */
+    int64_t rec_id_offset;
 } cols_t;
 
 static const cols_t *g_cols;
 
-static inline uint64_t vbits_of(const double *v, int64_t i) {
-    uint64_t b = 0;
-    if (v) memcpy(&b, &v[i], 8);
-    return b;
+static inline uint64_t gidx_of(const cols_t *c, int64_t i) {
+    return (uint64_t)(c->rec_ids ? c->rec_ids[i] : c->rec_id_offset + i);
 }
 
-/* order records by (pid, pk, value bits, index) */
+/* order records by (pid, pk, index) */
 static int cmp_rec(const void *a, const void *b) {
     int64_t i = *(const int64_t *)a, j = *(const int64_t *)b;
     const cols_t *c = g_cols;
     if (c->pid[i] != c->pid[j]) return c->pid[i] < c->pid[j] ? -1 : 1;
     if (c->pk[i] != c->pk[j]) return c->pk[i] < c->pk[j] ? -1 : 1;
-    uint64_t vi = vbits_of(c->v, i), vj = vbits_of(c->v, j);
-    if (vi != vj) return vi < vj ? -1 : 1;
     return i < j ? -1 : (i > j);
 }
 
@@ -197,44 +196,33 @@ static void emit_pair(const dpg_bound_params *p, const cols_t *c,
 }
 
 /* keep the `keep` records of sorted range [lo,hi) with the smallest record
- * priority; ranges are sorted by (pid, pk, vbits) so identical records are
- * adjacent and occ = position inside the run. Writes kept indices to dst. */
+ * priority philox(pid, pk, global record id).  Writes kept indices to dst. */
 static int64_t sample_records(uint64_t seed, const cols_t *c, const int64_t *ord,
-                              int64_t lo, int64_t hi, int64_t keep,
-                              int64_t *dst, uint64_t *tmpkey, int64_t *tmpidx) {
+                              int64_t lo, int64_t hi, int64_t keep, int64_t *dst) {
     int64_t n = hi - lo;
     if (n <= keep) {
         memcpy(dst, ord + lo, n * sizeof(int64_t));
         return n;
     }
-    uint32_t occ = 0;
+    /* selection of the `keep` smallest keys (ties: astronomically rare) via a
+     * full qsort on (key, position) pairs */
+    group_t *gs = (group_t *)malloc(n * sizeof(group_t));
     for (int64_t t = 0; t < n; ++t) {
         int64_t i = ord[lo + t];
-        if (t > 0) {
-            int64_t j = ord[lo + t - 1];
-            occ = (c->pid[i] == c->pid[j] && c->pk[i] == c->pk[j] &&
-                   vbits_of(c->v, i) == vbits_of(c->v, j)) ? occ + 1 : 0;
-        }
-        tmpkey[t] = rec_prio(seed, (uint32_t)c->pid[i], (uint32_t)c->pk[i],
-                             vbits_of(c->v, i), occ);
+        gs[t].key = rec_prio(seed, (uint64_t)c->pid[i], (uint32_t)c->pk[i], gidx_of(c, i));
+        gs[t].lo = t;
     }
-    /* selection of the `keep` smallest keys (ties: astronomically rare) */
-    for (int64_t t = 0; t < n; ++t) tmpidx[t] = t;
-    /* simple partial sort via full qsort on (key, t) pairs */
-    group_t *gs = (group_t *)malloc(n * sizeof(group_t));
-    for (int64_t t = 0; t < n; ++t) { gs[t].key = tmpkey[t]; gs[t].lo = t; }
     qsort(gs, n, sizeof(group_t), cmp_group);
     for (int64_t t = 0; t < keep; ++t) dst[t] = ord[lo + gs[t].lo];
     free(gs);
     return keep;
 }
 
-int dpo_bound_aggregate(uint64_t seed, const int64_t *pid, const int64_t *pk,
-                        const double *v, int64_t n, const dpg_bound_params *p,
-                        dpg_partials *out) {
-    cols_t c = {pid, pk, v};
+int dpo_bound_aggregate_ids(uint64_t seed, const int64_t *pid, const int64_t *pk,
+                            const double *v, const int64_t *rec_ids, int64_t n,
+                            const dpg_bound_params *p, dpg_partials *out) {
+    cols_t c = {pid, pk, v, rec_ids, p->rec_id_offset};
     for (int64_t i = 0; i < n; ++i) {
-        if (pid[i] < 0 || pid[i] > 0xFFFFFFFFll) return DPG_ERR_KEY_RANGE;
         if (pk[i] < 0 || pk[i] >= p->n_partitions) return DPG_ERR_KEY_RANGE;
     }
     int64_t *ord = (int64_t *)malloc((n + 1) * sizeof(int64_t));
@@ -249,8 +237,6 @@ int dpo_bound_aggregate(uint64_t seed, const int64_t *pid, const int64_t *pk,
     qsort(ord, nn, sizeof(int64_t), cmp_rec);
     int64_t *kept = (int64_t *)malloc((nn + 1) * sizeof(int64_t));
     int64_t *kept2 = (int64_t *)malloc((nn + 1) * sizeof(int64_t));
-    uint64_t *tkey = (uint64_t *)malloc((nn + 1) * sizeof(uint64_t));
-    int64_t *tidx = (int64_t *)malloc((nn + 1) * sizeof(int64_t));
     group_t *pairs = (group_t *)malloc((nn + 1) * sizeof(group_t));
 
     int64_t a = 0;
@@ -260,10 +246,8 @@ int dpo_bound_aggregate(uint64_t seed, const int64_t *pid, const int64_t *pk,
         /* [a,b) = all records of one privacy id */
         if (p->mode == DPG_MODE_PER_PRIVACY_ID) {
             /* contribution_bounders.py:108-150: sample <= L records per pid,
-             * then group the kept ones by partition. ord[a,b) is sorted by
-             * (pk, vbits) so occ is the position inside identical runs. */
-            int64_t m = sample_records(seed, &c, ord, a, b,
-                                       p->max_contributions, kept, tkey, tidx);
+             * then group the kept ones by partition. */
+            int64_t m = sample_records(seed, &c, ord, a, b, p->max_contributions, kept);
             /* regroup kept records by pk (kept is in priority order) */
             qsort(kept, m, sizeof(int64_t), cmp_rec);
             int64_t s = 0;
@@ -279,7 +263,7 @@ int dpo_bound_aggregate(uint64_t seed, const int64_t *pid, const int64_t *pk,
             while (s < b) {
                 int64_t e = s;
                 while (e < b && pk[ord[e]] == pk[ord[s]]) ++e;
-                uint32_t pp = pair_prio(seed, (uint32_t)pid[ord[s]],
+                uint32_t pp = pair_prio(seed, (uint64_t)pid[ord[s]],
                                         (uint32_t)pk[ord[s]]);
                 pairs[np].key = ((uint64_t)pp << 32) | (uint32_t)pk[ord[s]];
                 pairs[np].lo = s;
@@ -301,16 +285,21 @@ int dpo_bound_aggregate(uint64_t seed, const int64_t *pid, const int64_t *pk,
                 } else {
                     /* contribution_bounders.py:74-76: <= mcpp per pair */
                     int64_t m = sample_records(seed, &c, ord, lo, hi,
-                                               p->max_contributions_per_partition,
-                                               kept2, tkey, tidx);
+                                               p->max_contributions_per_partition, kept2);
                     emit_pair(p, &c, kept2, m, out);
                 }
             }
         }
         a = b;
     }
-    free(ord); free(kept); free(kept2); free(tkey); free(tidx); free(pairs);
+    free(ord); free(kept); free(kept2); free(pairs);
     return DPG_OK;
+}
+
+int dpo_bound_aggregate(uint64_t seed, const int64_t *pid, const int64_t *pk,
+                        const double *v, int64_t n, const dpg_bound_params *p,
+                        dpg_partials *out) {
+    return dpo_bound_aggregate_ids(seed, pid, pk, v, NULL, n, p, out);
 }
 
 /* ------------------------------------------------- selection + metrics */
@@ -410,12 +399,11 @@ int dpo_select_and_noise(uint64_t seed, const dpg_partials *in,
 }
 
 /* exported helpers for distribution tests */
-uint32_t dpo_pair_prio(uint64_t seed, uint32_t pid, uint32_t pk) {
+uint32_t dpo_pair_prio(uint64_t seed, uint64_t pid, uint32_t pk) {
     return pair_prio(seed, pid, pk);
 }
-uint64_t dpo_rec_prio(uint64_t seed, uint32_t pid, uint32_t pk, uint64_t vbits,
-                      uint32_t occ) {
-    return rec_prio(seed, pid, pk, vbits, occ);
+uint64_t dpo_rec_prio(uint64_t seed, uint64_t pid, uint32_t pk, uint64_t gidx) {
+    return rec_prio(seed, pid, pk, gidx);
 }
 double dpo_noise_sample(int kind, double x, double scale, uint64_t seed,
                         uint64_t pk, uint32_t slot) {

@@ -22,7 +22,9 @@ class _Bound(ctypes.Structure):
                 ("min_value", ctypes.c_double), ("max_value", ctypes.c_double),
                 ("min_sum_per_partition", ctypes.c_double),
                 ("max_sum_per_partition", ctypes.c_double),
-                ("n_partitions", ctypes.c_int64), ("public_mask", ctypes.c_void_p)]
+                ("n_partitions", ctypes.c_int64), ("public_mask", ctypes.c_void_p),
+                ("pid_min", ctypes.c_int64), ("pid_count", ctypes.c_int64),
+                ("rec_id_offset", ctypes.c_int64)]
 
 
 class _Partials(ctypes.Structure):
@@ -79,14 +81,17 @@ def lib():
         L.dpo_bound_aggregate.argtypes = [ctypes.c_uint64, vp, vp, vp, ctypes.c_int64,
                                           ctypes.POINTER(_Bound), ctypes.POINTER(_Partials)]
         L.dpo_bound_aggregate.restype = ctypes.c_int
+        L.dpo_bound_aggregate_ids.argtypes = [ctypes.c_uint64, vp, vp, vp, vp, ctypes.c_int64,
+                                              ctypes.POINTER(_Bound), ctypes.POINTER(_Partials)]
+        L.dpo_bound_aggregate_ids.restype = ctypes.c_int
         L.dpo_select_and_noise.argtypes = [ctypes.c_uint64, ctypes.POINTER(_Partials),
                                            ctypes.POINTER(_Select), ctypes.POINTER(_Noise),
                                            vp, vp]
         L.dpo_select_and_noise.restype = ctypes.c_int
-        L.dpo_pair_prio.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32]
+        L.dpo_pair_prio.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32]
         L.dpo_pair_prio.restype = ctypes.c_uint32
-        L.dpo_rec_prio.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
-                                   ctypes.c_uint64, ctypes.c_uint32]
+        L.dpo_rec_prio.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
+                                   ctypes.c_uint64]
         L.dpo_rec_prio.restype = ctypes.c_uint64
         L.dpo_noise_sample.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.c_double,
                                        ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32]
@@ -103,9 +108,12 @@ def _p(a):
     return a.ctypes.data if a is not None else None
 
 
-def bound_aggregate(pid, pk, value, fields: dict, seed: int, public_mask=None):
-    """Dense partials (numpy) of the bounded aggregation."""
+def bound_aggregate(pid, pk, value, fields: dict, seed: int, public_mask=None, rec_ids=None):
+    """Dense partials (numpy) of the bounded aggregation.  The record sampler
+    is keyed by the global record id: rec_ids[i] if given, else
+    fields['rec_id_offset'] (default 0) + i."""
     pid = np.ascontiguousarray(pid, dtype=np.int64)
+    rid = None if rec_ids is None else np.ascontiguousarray(rec_ids, dtype=np.int64)
     pk = np.ascontiguousarray(pk, dtype=np.int64)
     v = None if value is None else np.ascontiguousarray(value, dtype=np.float64)
     P = int(fields["n_partitions"])
@@ -118,8 +126,8 @@ def bound_aggregate(pid, pk, value, fields: dict, seed: int, public_mask=None):
         b.public_mask = pm.ctypes.data
     part = _Partials(P, _p(out["rows"]), _p(out["count"]), _p(out["sum"]),
                      _p(out["nsum"]), _p(out["nsq"]))
-    st = lib().dpo_bound_aggregate(ctypes.c_uint64(seed), _p(pid), _p(pk), _p(v), len(pid),
-                                   ctypes.byref(b), ctypes.byref(part))
+    st = lib().dpo_bound_aggregate_ids(ctypes.c_uint64(seed), _p(pid), _p(pk), _p(v), _p(rid),
+                                       len(pid), ctypes.byref(b), ctypes.byref(part))
     if st != 0:
         raise ValueError(f"oracle bound_aggregate failed with status {st}")
     return out
@@ -156,8 +164,9 @@ def pair_prio(seed, pid, pk):
     return lib().dpo_pair_prio(ctypes.c_uint64(seed), pid, pk)
 
 
-def rec_prio(seed, pid, pk, vbits, occ):
-    return lib().dpo_rec_prio(ctypes.c_uint64(seed), pid, pk, ctypes.c_uint64(vbits), occ)
+def rec_prio(seed, pid, pk, gidx):
+    return lib().dpo_rec_prio(ctypes.c_uint64(seed), ctypes.c_uint64(pid), pk,
+                              ctypes.c_uint64(gidx))
 
 
 def noise_sample(kind, x, scale, seed, pk, slot):

@@ -29,7 +29,9 @@ class BoundParams(ctypes.Structure):
                 ("min_value", ctypes.c_double), ("max_value", ctypes.c_double),
                 ("min_sum_per_partition", ctypes.c_double),
                 ("max_sum_per_partition", ctypes.c_double),
-                ("n_partitions", ctypes.c_int64), ("public_mask", ctypes.c_void_p)]
+                ("n_partitions", ctypes.c_int64), ("public_mask", ctypes.c_void_p),
+                ("pid_min", ctypes.c_int64), ("pid_count", ctypes.c_int64),
+                ("rec_id_offset", ctypes.c_int64)]
 
 
 class Partials(ctypes.Structure):

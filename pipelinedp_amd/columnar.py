@@ -10,20 +10,20 @@ same extractors but prefers columnar input:
 * Any other iterable is treated as rows; the extractors run per row on the
   host (reference behaviour, slow, meant for small inputs).
 
-Keys: the kernels need privacy ids in [0, 2^32-1) and dense partition ids
-in [0, P).  Integer keys that already satisfy this are used as they are;
-anything else (strings, tuples, huge or negative ints) is dictionary-encoded
-(`unique` + inverse), and the partition dictionary maps results back.
-Encoding is ingest, not part of the DP computation.
+Keys: the kernels need integer privacy ids spanning at most 2^32 values and
+dense partition ids in [0, P).  Integer keys that already satisfy this are
+used as they are; anything else (strings, tuples, ints spread wider) is
+dictionary-encoded (`unique` + inverse), and the partition dictionary maps
+results back.  Encoding is ingest, not part of the DP computation.
 """
 import dataclasses
 from collections.abc import Mapping
-from typing import Any, Optional, Sequence
+from typing import Any, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
 
-_PID_LIMIT = 0xFFFFFFFF  # exclusive
+_PID_SPAN = 1 << 32  # privacy ids of one call must span at most 2^32 values
 
 
 @dataclasses.dataclass
@@ -32,11 +32,19 @@ class ColumnarData:
 
     `n_partitions`: if given, `pk` must already hold dense ids in
     [0, n_partitions) and is passed to the device unchecked (the kernel still
-    rejects out-of-range keys with ValueError)."""
+    rejects out-of-range keys with ValueError).
+
+    `privacy_id_range`: optional (lo, hi) with every privacy id in [lo, hi),
+    hi - lo <= 2^32; saves the device a min/max pass (out-of-range ids raise
+    ValueError).  `record_id_offset`: global id of record 0 -- the record
+    sampler is keyed by (pid, pk, record id), so the shards of one dataset,
+    each given its offset, sample exactly like the whole."""
     pid: Any = None
     pk: Any = None
     value: Any = None
     n_partitions: Optional[int] = None
+    privacy_id_range: Optional[Tuple[int, int]] = None
+    record_id_offset: int = 0
 
     def __getitem__(self, name):
         return getattr(self, name)
@@ -58,6 +66,9 @@ class EncodedInput:
     key_table: Optional[Sequence]  # dense id -> original key (None: identity)
     public_mask: Optional[torch.Tensor] = None  # uint8 bitmap on the device
     public_count: int = 0
+    pid_min: int = 0
+    pid_count: int = 0        # 0: unknown (the device reduces min / max)
+    rec_id_offset: int = 0
 
 
 def _extract(col, extractor):
@@ -121,11 +132,14 @@ def _range(t: torch.Tensor):
 
 def encode(col, extractors, device: torch.device, need_values: bool,
            public_partitions=None, need_pid: bool = True) -> EncodedInput:
+    pid_range, rec_off = None, 0
     if _is_columnar(col):
         pid = _extract(col, extractors.privacy_id_extractor) if need_pid else None
         pk = _extract(col, extractors.partition_extractor)
         value = _extract(col, extractors.value_extractor) if need_values else None
         hint = col.n_partitions if isinstance(col, ColumnarData) else col.get("n_partitions")
+        if isinstance(col, ColumnarData):
+            pid_range, rec_off = col.privacy_id_range, int(col.record_id_offset)
     else:
         rows = col if isinstance(col, list) else list(col)
         ex = extractors
@@ -174,27 +188,39 @@ def encode(col, extractors, device: torch.device, need_values: bool,
         pk_ids, key_table, public_ids = _encode_keys(pk, device, public_list)
         P = max(len(key_table), 1)
 
-    # ---- privacy ids -> [0, 2^32-1)
+    # ---- privacy ids -> integers spanning <= 2^32 values, with their range
+    # when known (else the device reduces it)
     pid_ids = None
+    pid_min, pid_count = 0, 0
     if need_pid:
         if pid is None:
             raise ValueError("privacy_id_extractor must be set")
         if _integer_like(pid):
             pid_t = _to_tensor(pid, device).to(torch.int64)
-            if hint is None:
+            if pid_range is not None:
+                lo, hi = int(pid_range[0]), int(pid_range[1])
+                if not 0 < hi - lo <= _PID_SPAN:
+                    raise ValueError("privacy_id_range must be (lo, hi) with 0 < hi - lo <= 2^32")
+                pid_min, pid_count = lo, hi - lo
+            elif hint is None and n > 0:
                 lo, hi = _range(pid_t)
-                if lo < 0 or hi >= _PID_LIMIT:
-                    pid_t, _, _ = _encode_keys(pid_t, device)
+                if hi - lo >= _PID_SPAN:
+                    pid_t, uniq, _ = _encode_keys(pid_t, device)
+                    pid_min, pid_count = 0, max(1, len(uniq))
+                else:
+                    pid_min, pid_count = lo, hi - lo + 1
             pid_ids = pid_t
         else:
-            pid_ids, _, _ = _encode_keys(pid, device)
+            pid_ids, table, _ = _encode_keys(pid, device)
+            pid_min, pid_count = 0, max(1, len(table))
 
     val = None
     if need_values:
         val = _to_tensor(value, device).to(torch.float64)
 
     enc = EncodedInput(pid=pid_ids, pk=pk_ids.contiguous(), value=val, n=n,
-                       n_partitions=int(P), key_table=key_table)
+                       n_partitions=int(P), key_table=key_table, pid_min=pid_min,
+                       pid_count=pid_count, rec_id_offset=rec_off)
     if public_ids is not None:
         mask = np.zeros((P + 7) // 8, dtype=np.uint8)
         ids = np.unique(np.asarray(public_ids, dtype=np.int64))

@@ -2,22 +2,25 @@
 // hot path.  Build: hipcc --offload-arch=gfx950 -O3 -shared -fPIC.
 //
 // Pipeline of dpg_bound_aggregate (DESIGN.md "Kernels"):
-//   partition levels (hist, scan, digit base, scatter) by privacy-id hash
-//   -> k_make_chunks (greedy packing of fine buckets), refine level for
-//      oversize buckets -> k_bound_chunks (+ k_bound_global for single
-//      buckets still over the chunk capacity)
+//   [pid range reduction when the caller does not declare it]
+//   level 1: SoA (pid, pk) -> packed records (key residual, record index),
+//            bucketed by the top b1 <= 10 bits of hk(pid)
+//   level 2: records -> buckets by the next b2 <= 11 hash bits (~512 records)
+//   -> k_make_chunks (greedy packing of fine buckets into <= 1024-record
+//      chunks), refine level for oversize buckets -> k_bound_chunks
+//      (+ k_bound_big for single buckets still over the chunk capacity)
 //   -> one partition-key-range level over the kept pairs -> k_reduce_items
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <chrono>
-#include <cstdlib>
-#include <thread>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "dpg_bound.h"
@@ -30,11 +33,9 @@ using namespace dpg;
 
 namespace {
 
-constexpr int kCap16 = 2048;   // chunk capacity (records) of the COUNT/SUM kernel
-constexpr int kCap32 = 1536;   // chunk capacity of the MEAN/VARIANCE kernel
-constexpr uint32_t kBucketCap = 2048;
-constexpr uint32_t kChunkGroup = 32;  // fine buckets per packing thread
-constexpr int kMaxLevels = 3;
+constexpr uint32_t kBucketTarget = 512;  // average records per fine bucket
+constexpr uint32_t kMaxB1 = 10, kMaxB2 = 11;
+constexpr uint32_t kChunkGroup = 32;     // fine buckets per packing thread
 
 struct Buf {
     void *p = nullptr;
@@ -43,19 +44,16 @@ struct Buf {
 
 struct Control {  // device-side counters, zeroed per call
     uint32_t err;
-    uint32_t queue;
     uint32_t item_cursor;
-    uint32_t n_oversize;  // buckets left for the global-memory path
     uint32_t ntiles[8];
-    int64_t nvalid;
     int64_t n_scalar;
-    int64_t kept_total;
     uint32_t n_chunks;
-    uint32_t n_over;      // fine buckets over the chunk capacity
-    uint32_t n_over2;     // refined buckets still over it
+    uint32_t n_over;   // fine buckets over the chunk capacity
+    uint32_t n_over2;  // refined buckets still over it
     uint32_t pad0;
     unsigned long long over_records;
     unsigned long long over2_records;
+    unsigned long long pid_lo, pid_hi;  // order-preserving (x ^ 2^63) min / max
 };
 
 }  // namespace
@@ -70,8 +68,8 @@ struct dpg_ctx {
     std::vector<hipEvent_t> events;
     int n_events_used = 0;
     hipStream_t last_stream = nullptr;
-    uint32_t bucket_target = 0;  // 0: half the chunk capacity
-    uint32_t bucket_cap = kBucketCap;
+    uint32_t bucket_target = 0;  // 0: kBucketTarget
+    uint32_t bucket_cap = kBCap;
 };
 
 namespace {
@@ -148,7 +146,7 @@ void *ws(dpg_ctx *ctx, const char *name, size_t bytes, int *status) {
     T *ptr = reinterpret_cast<T *>(ws(ctx, name, sizeof(T) * (size_t)(count), &st)); \
     if (!ptr) return st;
 
-void stage(dpg_ctx *ctx, hipStream_t s, const char *name) {
+void stage(dpg_ctx *ctx, hipStream_t s, const std::string &name) {
     if (ctx->n_events_used >= (int)ctx->events.size()) {
         hipEvent_t e;
         (void)hipEventCreate(&e);
@@ -158,21 +156,47 @@ void stage(dpg_ctx *ctx, hipStream_t s, const char *name) {
     ctx->stage_names.push_back(name);
 }
 
-uint32_t ceil_log2(double x) {
-    if (x <= 1.0) return 0;
-    return (uint32_t)std::ceil(std::log2(x));
+// bits needed to index `count` distinct values (0 for count <= 1)
+uint32_t bits_for(uint64_t count) {
+    uint32_t b = 0;
+    while (b < 64 && (count - 1) >> b) ++b;
+    return count <= 1 ? 0 : b;
 }
 
-// One partition level over `S` segments of `in` (or the SoA input).
-template <class Src, class Rec, class Dig, int IPT>
-int run_level(dpg_ctx *ctx, hipStream_t s, Src src, Dig dig, uint32_t S, const int64_t *seg_start,
+uint64_t low_mask(uint32_t bits) { return bits >= 64 ? ~0ull : ((1ull << bits) - 1ull); }
+
+// pid range of the input (order-preserving unsigned atomics)
+__global__ void k_pid_minmax(const int64_t *pid, int64_t n, unsigned long long *lo,
+                             unsigned long long *hi) {
+    unsigned long long a = ~0ull, b = 0ull;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const unsigned long long x = (unsigned long long)pid[i] ^ 0x8000000000000000ull;
+        a = x < a ? x : a;
+        b = x > b ? x : b;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long c = __shfl_xor(a, o, 64), d = __shfl_xor(b, o, 64);
+        a = c < a ? c : a;
+        b = d > b ? d : b;
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMin(lo, a);
+        atomicMax(hi, b);
+    }
+}
+
+// One partition level over `S` segments of the source.
+template <class Src, class Rec, int IPT, int FMAX>
+int run_level(dpg_ctx *ctx, hipStream_t s, const Src &src, uint32_t S, const int64_t *seg_start,
               const uint32_t *seg_cnt, const int64_t *seg_cnt64, int64_t n_upper, uint32_t F,
               uint32_t bits, Rec *out, const char *tag, int64_t **base_out, uint32_t **tot_out,
               uint32_t *ntiles_dev, const int64_t *out_start = nullptr) {
     int st = DPG_OK;
+    if (F > (uint32_t)FMAX) return fail(ctx, DPG_ERR_HIP, "internal: digit fan-out too large");
     const int64_t sub = (int64_t)kPartThreads * IPT;
-    int64_t tile = std::max<int64_t>(sub, ((n_upper / 3072 + sub - 1) / sub) * sub);
-    uint32_t max_tiles = (uint32_t)(n_upper / tile + S + 1);
+    const int64_t tile = std::max<int64_t>(sub, ((n_upper / 3072 + sub - 1) / sub) * sub);
+    const uint32_t max_tiles = (uint32_t)(n_upper / tile + S + 1);
     std::string t(tag);
     WS(tiles, TileDesc, (t + ".tiles").c_str(), max_tiles);
     WS(stb, uint32_t, (t + ".stb").c_str(), S);
@@ -180,28 +204,40 @@ int run_level(dpg_ctx *ctx, hipStream_t s, Src src, Dig dig, uint32_t S, const i
     WS(hist, uint32_t, (t + ".hist").c_str(), (size_t)max_tiles * F);
     WS(tot, uint32_t, (t + ".tot").c_str(), (size_t)S * F);
     WS(base, int64_t, (t + ".base").c_str(), (size_t)S * F);
+    stage(ctx, s, (t + ":hist").c_str());
     k_build_tiles<<<(S + 255) / 256, 256, 0, s>>>(seg_start, seg_cnt, seg_cnt64, S, tile, tiles, stb,
                                                   snt, ntiles_dev);
     LAUNCH_CHECK();
-    auto hsrc = hist_view(src);
-    k_hist<decltype(hsrc), Rec, Dig><<<max_tiles, kPartThreads, 4 * F * sizeof(uint32_t), s>>>(
-        hsrc, dig, tiles, ntiles_dev, F, hist);
+    k_hist<Src><<<max_tiles, kPartThreads, 4 * F * sizeof(uint32_t), s>>>(src, tiles, ntiles_dev,
+                                                                          F, hist);
     LAUNCH_CHECK();
     k_scan_tiles<<<dim3(S, (F + 63) / 64), 1024, 0, s>>>(stb, snt, F, hist, tot);
     LAUNCH_CHECK();
-    k_digit_base<<<S, 1024, 0, s>>>(out_start ? out_start : seg_start, F, tot, base, nullptr);
+    k_digit_base<<<S, 1024, 0, s>>>(out_start ? out_start : seg_start, F, tot, base);
     LAUNCH_CHECK();
-    size_t lds = sizeof(Rec) * sub + 1024 * 4 * 2 + 1024 * 8 + 16 * 4;
-    k_scatter<Src, Rec, Dig, IPT><<<max_tiles, kPartThreads, lds, s>>>(src, dig, tiles, ntiles_dev,
-                                                                      F, bits, hist, base, out);
+    constexpr size_t lds = scatter_lds<Src, Rec, IPT, FMAX>();
+    static_assert(lds <= 160 * 1024, "scatter LDS");
+    (void)hipFuncSetAttribute((const void *)k_scatter<Src, Rec, IPT, FMAX>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    stage(ctx, s, (t + ":scatter").c_str());
+    k_scatter<Src, Rec, IPT, FMAX><<<max_tiles, kPartThreads, lds, s>>>(src, tiles, ntiles_dev, F,
+                                                                         bits, hist, base, out);
     LAUNCH_CHECK();
     *base_out = base;
     *tot_out = tot;
     return DPG_OK;
 }
 
+// sub-tile sizes per record size: level 1 stages a 2-byte digit beside the
+// record; later levels recompute it
+template <class R>
+struct Ipt {
+    static constexpr int L1 = sizeof(R) == 8 ? 12 : 6;
+    static constexpr int LN = sizeof(R) == 8 ? 16 : 8;
+};
+
 BoundParams to_bound(const dpg_bound_params *p, uint64_t seed) {
-    BoundParams b;
+    BoundParams b{};
     b.mode = p->mode;
     b.sum_mode = p->sum_mode;
     b.mask = p->metric_mask;
@@ -215,48 +251,58 @@ BoundParams to_bound(const dpg_bound_params *p, uint64_t seed) {
     b.hi_pp = p->max_sum_per_partition;
     b.mid = p->min_value + (p->max_value - p->min_value) / 2;
     b.seed = seed;
+    b.rec_base = p->rec_id_offset;
     return b;
 }
 
-template <class Item>
-int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Rec16 *recs, const int64_t *bstart,
-                     const uint32_t *bcnt, uint32_t B, uint32_t hash_bits_left,
-                     const BoundParams &bp, Item *items, Item *items2, int64_t n, int64_t P,
-                     const dpg_partials *out, Control *ctl) {
+struct Plan {
+    uint32_t b1, b2, kbits, pkbits;
+    int64_t P;
+};
+
+// Bounding of the fine buckets + merge of the kept pairs per partition.
+template <class R, class KeyT, class Item>
+int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
+                     const int64_t *bstart, const uint32_t *bcnt, uint32_t B,
+                     const BoundParams &bp, int64_t n, const dpg_partials *out, Control *ctl) {
     int st = DPG_OK;
-    constexpr int kCap = ItemTraits<Item>::var ? kCap32 : kCap16;
-    using CL = ChunkLayout<Item, kCap>;
-    const uint32_t cap = std::min<uint32_t>(ctx->bucket_cap, (uint32_t)kCap);
-    // ---- pack fine buckets into chunks
+    using CL = ChunkLayout<KeyT, Item>;
+    const uint32_t cap = std::min<uint32_t>(ctx->bucket_cap, (uint32_t)kBCap);
+    const Fmt f = bp.fmt;
+    // ---- pack fine buckets into chunks (groups never span level-1 buckets)
     stage(ctx, s, "chunks");
-    WS(chunks, uint2, "chunks", B);
+    WS(chunks, uint4, "chunks", B);
     WS(ostart, int64_t, "over.start", B);
     WS(ocnt, uint32_t, "over.cnt", B);
-    const uint32_t ngroups = (B + kChunkGroup - 1) / kChunkGroup;
-    k_make_chunks<<<(ngroups + 255) / 256, 256, 0, s>>>(bstart, bcnt, B, kChunkGroup, cap, 0u,
-                                                         chunks, &ctl->n_chunks, ostart, ocnt,
-                                                         &ctl->n_over, &ctl->over_records);
+    WS(od1, uint32_t, "over.d1", B);
+    const uint32_t group = std::min<uint32_t>(kChunkGroup, 1u << pl.b2);
+    const uint32_t ngroups = (B + group - 1) / group;
+    k_make_chunks<<<(ngroups + 255) / 256, 256, 0, s>>>(bstart, bcnt, B, group, cap, 0u, pl.b2,
+                                                         nullptr, chunks, &ctl->n_chunks, ostart,
+                                                         ocnt, od1, &ctl->n_over,
+                                                         &ctl->over_records);
     LAUNCH_CHECK();
     Control hctl;
     HIP_TRY(hipMemcpyAsync(&hctl, ctl, sizeof(Control), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     if (hctl.err & 1u)
         return fail(ctx, DPG_ERR_KEY_RANGE,
-                    "privacy id outside [0, 2^32-1) or partition key outside [0, P)");
-    const uint2 *chunk_list = chunks;
-    const Rec16 *refined = recs;
-    // global-memory leftovers: (buffer, starts, counts, number)
-    const Rec16 *g_base = recs;
+                    "privacy id outside its declared range or partition key outside [0, P)");
+    const uint4 *chunk_list = chunks;
+    const R *refined = recs;
+    // global-memory leftovers: (buffer, starts, counts, level-1 buckets, number)
+    const R *g_base = recs;
     const int64_t *g_start = ostart;
     const uint32_t *g_cnt = ocnt;
+    const uint32_t *g_d1 = od1;
     uint32_t n_global = 0;
     if (hctl.n_over > 0) {
-        const uint32_t rbits = std::min<uint32_t>(10u, hash_bits_left);
+        const uint32_t left = pl.kbits - pl.b1 - pl.b2;  // hash bits not yet used
+        const uint32_t rbits = std::min<uint32_t>(kMaxB2, left);
         if (rbits == 0) {
             n_global = hctl.n_over;
         } else {
             // ---- refine oversize buckets by further privacy-id hash bits
-            stage(ctx, s, "refine");
             const uint32_t no = hctl.n_over, F2 = 1u << rbits;
             std::vector<uint32_t> hc(no);
             HIP_TRY(hipMemcpy(hc.data(), ocnt, no * 4, hipMemcpyDeviceToHost));
@@ -265,24 +311,27 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Rec16 *recs, const int64
             for (uint32_t i = 0; i < no; ++i) hout[i] = acc, acc += hc[i];
             WS(oout, int64_t, "over.out", no);
             HIP_TRY(hipMemcpyAsync(oout, hout.data(), no * 8, hipMemcpyHostToDevice, s));
-            WS(rbuf, Rec16, "refined", std::max<int64_t>(acc, 1));
+            WS(rbuf, R, "refined", std::max<int64_t>(acc, 1));
             int64_t *base2;
             uint32_t *tot2;
-            DigPid dig{hash_bits_left - rbits, F2 - 1};
-            int r = run_level<SrcAoS<Rec16>, Rec16, DigPid, kItemsPerThread>(
-                ctx, s, SrcAoS<Rec16>{recs}, dig, no, ostart, ocnt, nullptr, acc, F2, rbits, rbuf,
-                "refine", &base2, &tot2, &ctl->ntiles[3], oout);
+            const uint32_t shift = pl.pkbits + (pl.kbits - pl.b1) - pl.b2 - rbits;
+            SrcAoS<R> src{recs, f, shift, F2 - 1};
+            int r = run_level<SrcAoS<R>, R, Ipt<R>::LN, 2048>(ctx, s, src, no, ostart, ocnt,
+                                                               nullptr, acc, F2, rbits, rbuf,
+                                                               "refine", &base2, &tot2,
+                                                               &ctl->ntiles[3], oout);
             if (r) return r;
             const uint32_t B2 = no * F2;
-            WS(chunks2, uint2, "chunks.r", (size_t)hctl.n_chunks + B2);
-            HIP_TRY(hipMemcpyAsync(chunks2, chunks, (size_t)hctl.n_chunks * sizeof(uint2),
+            WS(chunks2, uint4, "chunks.r", (size_t)hctl.n_chunks + B2);
+            HIP_TRY(hipMemcpyAsync(chunks2, chunks, (size_t)hctl.n_chunks * sizeof(uint4),
                                    hipMemcpyDeviceToDevice, s));
             WS(o2start, int64_t, "over2.start", B2);
             WS(o2cnt, uint32_t, "over2.cnt", B2);
-            const uint32_t ng2 = (B2 + F2 - 1) / F2;
-            k_make_chunks<<<(ng2 + 255) / 256, 256, 0, s>>>(base2, tot2, B2, F2, cap, 1u, chunks2,
-                                                           &ctl->n_chunks, o2start, o2cnt,
-                                                           &ctl->n_over2, &ctl->over2_records);
+            WS(o2d1, uint32_t, "over2.d1", B2);
+            k_make_chunks<<<(no + 255) / 256, 256, 0, s>>>(base2, tot2, B2, F2, cap, 1u, rbits,
+                                                          od1, chunks2, &ctl->n_chunks, o2start,
+                                                          o2cnt, o2d1, &ctl->n_over2,
+                                                          &ctl->over2_records);
             LAUNCH_CHECK();
             HIP_TRY(hipMemcpyAsync(&hctl, ctl, sizeof(Control), hipMemcpyDeviceToHost, s));
             HIP_TRY(hipStreamSynchronize(s));
@@ -291,12 +340,14 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Rec16 *recs, const int64
             g_base = rbuf;
             g_start = o2start;
             g_cnt = o2cnt;
+            g_d1 = o2d1;
             n_global = hctl.n_over2;
         }
     }
     // ---- bounding of every chunk in LDS; workgroup g writes its items to
     // items[wg_off[g], ...), the global-memory path after all of them
-    const uint32_t G = (uint32_t)std::min(ctx->n_cu, 1022);
+    const uint32_t G = (uint32_t)std::min(ctx->n_cu * CL::PER_CU, 1022);
+    WS(items, Item, "items", std::max<int64_t>(n, 1));
     WS(wg_rec, uint32_t, "wg.rec", G + 1);
     WS(wg_off, int64_t, "wg.off", G + 2);
     WS(wg_cnt, uint32_t, "wg.cnt", G + 1);
@@ -306,7 +357,6 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Rec16 *recs, const int64
     k_scan_small<<<1, 1024, 0, s>>>(wg_rec, G, wg_off, nullptr);
     LAUNCH_CHECK();
     HIP_TRY(hipMemsetAsync(wg_cnt + G, 0, 4, s));
-    stage(ctx, s, "bound");
     BoundParams bpl = bp;
     uint32_t *prog = watchdog_seconds() ? watchdog_buffer(G) : nullptr;
     bpl.progress = prog;
@@ -317,22 +367,26 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Rec16 *recs, const int64
         HIP_TRY(hipMemsetAsync(pc, 0, 16 * 8, s));
         bpl.phase_cyc = pc;
     }
-    k_bound_chunks<Item, kCap><<<G, kChunkThreads, CL::TOTAL, s>>>(
-        recs, refined, chunk_list, &ctl->n_chunks, bpl, items, wg_off, wg_cnt);
+    (void)hipFuncSetAttribute((const void *)k_bound_chunks<KeyT, Item, R>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)CL::TOTAL);
+    stage(ctx, s, "bound");
+    k_bound_chunks<KeyT, Item, R><<<G, kBT, CL::TOTAL, s>>>(recs, refined, chunk_list,
+                                                           &ctl->n_chunks, bpl, items, wg_off,
+                                                           wg_cnt);
     LAUNCH_CHECK();
     stage(ctx, s, "bound.tail");
     if (prog) watchdog_wait(s, prog, G, "k_bound_chunks");
     if (timing) {
         unsigned long long h[16];
         HIP_TRY(hipMemcpy(h, bpl.phase_cyc, sizeof(h), hipMemcpyDeviceToHost));
-        static const char *nm[9] = {"-", "-", "A1.insert", "A2.lists", "C1.alloc",
-                                    "C2C3.mpc", "D.mcpp", "E.acc", "F.emit"};
+        static const char *nm[9] = {"-", "-", "A.insert", "B.slots", "C.mpc",
+                                    "D.state", "E.mcpp", "F.acc", "G.emit"};
         unsigned long long tot = 0;
         for (int i = 2; i <= 8; ++i) tot += h[i];
         std::fprintf(stderr, "[dpg phase] chunks=%u over=%u over2=%u per-WG Mcycles:",
                      hctl.n_chunks, hctl.n_over, hctl.n_over2);
         for (int i = 2; i <= 8; ++i)
-            std::fprintf(stderr, " %s=%.3f(%.0f%%)", nm[i], h[i] / 1e6 / ctx->n_cu,
+            std::fprintf(stderr, " %s=%.3f(%.0f%%)", nm[i], h[i] / 1e6 / G,
                          100.0 * h[i] / (tot ? tot : 1));
         std::fprintf(stderr, "\n");
     }
@@ -344,7 +398,7 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Rec16 *recs, const int64
         size_t total = 0;
         for (uint32_t i = 0; i < n_global; ++i) {
             off[i] = total;
-            total += align16(BucketLayout::make(cnt[i], ItemTraits<Item>::var, 4).total);
+            total += align16(BigLayout::make(cnt[i], ItemTraits<Item>::var).total);
         }
         WS(scratch, char, "bound.scratch", total);
         WS(doff, size_t, "bound.scratch_off", n_global);
@@ -356,34 +410,36 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Rec16 *recs, const int64
         bpg.phase_cyc = nullptr;
         if (watchdog_seconds())
             std::fprintf(stderr, "[dpg] %u oversize buckets, scratch %zu bytes\n", n_global, total);
-        k_bound_global<Item><<<n_global, kBoundThreads, 0, s>>>(g_base, g_start, g_cnt, doff,
-                                                                scratch, bpg, items, wg_off + G,
-                                                                wg_cnt + G);
+        k_bound_big<Item, R><<<n_global, kBigThreads, 0, s>>>(g_base, g_start, g_cnt, g_d1, doff,
+                                                              scratch, bpg, items, wg_off + G,
+                                                              wg_cnt + G);
         LAUNCH_CHECK();
-        if (gprog) watchdog_wait(s, gprog, n_global, "k_bound_global");
+        if (gprog) watchdog_wait(s, gprog, n_global, "k_bound_big");
     }
     k_scan_small<<<1, 1024, 0, s>>>(wg_cnt, G + 1, wg_pre, &ctl->item_cursor);
     LAUNCH_CHECK();
     HIP_TRY(hipMemcpyAsync(&hctl, ctl, sizeof(Control), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     if (hctl.err & 2u) return fail(ctx, DPG_ERR_HIP, "internal hash-table error in bounding");
-    const SrcSeg<Item> item_src{items, wg_pre, wg_off, G + 1};
+    const int64_t n_items = hctl.item_cursor;
+    const SrcSeg<Item> item_src{items, wg_pre, wg_off, G + 1, (uint32_t)kRangeBits};
     // ---- merge kept pairs per partition
-    stage(ctx, s, "reduce");
     Partials po{out->rows, out->count, out->sum, out->nsum, out->nsq};
+    const int64_t P = pl.P;
     const int64_t nranges = (P + kRange - 1) / kRange;
-    if (nranges <= 1024) {
+    if (n_items > 0 && nranges <= 1024) {
         uint32_t F = (uint32_t)std::max<int64_t>(1, nranges);
-        uint32_t bits = std::max<uint32_t>(1, ceil_log2((double)F));
+        uint32_t bits = std::max<uint32_t>(1, bits_for(F));
         int64_t *baseR;
         uint32_t *totR;
-        int r = run_level<SrcSeg<Item>, Item, DigPk<Item>, (sizeof(Item) == 16 ? 8 : 4)>(
-            ctx, s, item_src, DigPk<Item>{(uint32_t)kRangeBits}, 1u, nullptr,
-            &ctl->item_cursor, nullptr, n, F, bits, items2, "items", &baseR, &totR,
-            &ctl->ntiles[4]);
+        WS(items2, Item, "items2", n_items);
+        int r = run_level<SrcSeg<Item>, Item, (sizeof(Item) == 16 ? 8 : 4), 1024>(
+            ctx, s, item_src, 1u, nullptr, &ctl->item_cursor, nullptr, n_items, F, bits, items2,
+            "items", &baseR, &totR, &ctl->ntiles[4]);
         if (r) return r;
+        stage(ctx, s, "reduce");
         const int64_t rtile = 65536;
-        uint32_t max_tiles = (uint32_t)(n / rtile + F + 1);
+        uint32_t max_tiles = (uint32_t)(n_items / rtile + F + 1);
         WS(rt, TileDesc, "reduce.tiles", max_tiles);
         WS(rstb, uint32_t, "reduce.stb", F);
         WS(rsnt, uint32_t, "reduce.snt", F);
@@ -393,13 +449,64 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Rec16 *recs, const int64
         size_t lds_r = (size_t)kRange * (ItemTraits<Item>::var ? 3 * 8 : 8) + kRange * 8;
         k_reduce_items<Item><<<max_tiles, 1024, lds_r, s>>>(items2, rt, &ctl->ntiles[5], P, po);
         LAUNCH_CHECK();
-    } else {
+    } else if (n_items > 0) {
         k_reduce_items_direct<Item, SrcSeg<Item>><<<ctx->n_cu * 8, 256, 0, s>>>(
             item_src, &ctl->item_cursor, po);
         LAUNCH_CHECK();
     }
     stage(ctx, s, "end");
     return DPG_OK;
+}
+
+template <class R>
+int pipeline(dpg_ctx *ctx, hipStream_t s, const int64_t *pid, const int64_t *pk,
+             const double *value, int64_t n, const dpg_bound_params *p, const dpg_partials *out,
+             Control *ctl, const Plan &pl, int64_t pid_min, uint64_t U, uint32_t ib) {
+    int st = DPG_OK;
+    const bool var = (p->metric_mask & (DPG_M_MEAN | DPG_M_VARIANCE)) != 0;
+    WS(recA, R, "recA", n);
+    WS(recB, R, "recB", n);
+    const Fmt f{ib, pl.pkbits, pl.kbits, pl.b1};
+    const HashK H = make_hash(pl.kbits);
+    // ---- level 1: SoA -> records bucketed by the top b1 hash bits
+    const uint32_t F1 = 1u << pl.b1;
+    SrcSoAKey<R> s1{pid, pk, p->public_mask, pl.P, pid_min, U, H, f,
+                    low_mask(pl.kbits - pl.b1 + pl.pkbits), pl.kbits - pl.b1, &ctl->err};
+    int64_t *bstart = nullptr;
+    uint32_t *bcnt = nullptr;
+    int r = run_level<SrcSoAKey<R>, R, Ipt<R>::L1, 1024>(ctx, s, s1, 1u, nullptr, nullptr,
+                                                         &ctl->n_scalar, n, F1, pl.b1, recA,
+                                                         "partition1", &bstart, &bcnt, &ctl->ntiles[0]);
+    if (r) return r;
+    const R *cur = recA;
+    uint32_t B = F1;
+    if (pl.b2 > 0) {
+        // ---- level 2: next b2 hash bits inside every level-1 bucket
+        const uint32_t F2 = 1u << pl.b2;
+        SrcAoS<R> s2{recA, f, pl.pkbits + (pl.kbits - pl.b1) - pl.b2, F2 - 1};
+        r = run_level<SrcAoS<R>, R, Ipt<R>::LN, 2048>(ctx, s, s2, F1, bstart, bcnt, nullptr, n, F2,
+                                                       pl.b2, recB, "partition2", &bstart, &bcnt,
+                                                       &ctl->ntiles[1]);
+        if (r) return r;
+        cur = recB;
+        B = F1 * F2;
+    }
+    BoundParams bp = to_bound(p, ctx->seed);
+    bp.fmt = f;
+    bp.hash = H;
+    bp.pid_min = pid_min;
+    bp.value = value;
+    bp.err = &ctl->err;
+    const bool key32 = pl.pkbits <= 21;  // (pid slot < 2^10) << pkbits | pk < 2^31
+    if (var)
+        return key32 ? bound_and_reduce<R, uint32_t, Item32>(ctx, s, pl, cur, bstart, bcnt, B, bp,
+                                                             n, out, ctl)
+                     : bound_and_reduce<R, uint64_t, Item32>(ctx, s, pl, cur, bstart, bcnt, B, bp,
+                                                             n, out, ctl);
+    return key32 ? bound_and_reduce<R, uint32_t, Item16>(ctx, s, pl, cur, bstart, bcnt, B, bp, n,
+                                                         out, ctl)
+                 : bound_and_reduce<R, uint64_t, Item16>(ctx, s, pl, cur, bstart, bcnt, B, bp, n,
+                                                         out, ctl);
 }
 
 }  // namespace
@@ -413,11 +520,6 @@ dpg_ctx *dpg_ctx_create(int device, uint64_t seed) {
     c->seed = seed;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->n_cu = prop.multiProcessorCount;
-    // the bound kernel needs ~150 KB of dynamic LDS
-    (void)hipFuncSetAttribute((const void *)k_bound_chunks<Item16, kCap16>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void *)k_bound_chunks<Item32, kCap32>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     return c;
 }
 
@@ -445,7 +547,7 @@ int dpg_set_seed(dpg_ctx *c, uint64_t seed) {
 int dpg_set_tuning(dpg_ctx *ctx, int32_t bucket_target, int32_t bucket_cap) {
     if (!ctx) return DPG_ERR_INVALID_ARG;
     if (bucket_target > 0) ctx->bucket_target = (uint32_t)bucket_target;
-    if (bucket_cap > 0) ctx->bucket_cap = std::min<uint32_t>((uint32_t)bucket_cap, kBucketCap);
+    if (bucket_cap > 0) ctx->bucket_cap = std::min<uint32_t>((uint32_t)bucket_cap, kBCap);
     return DPG_OK;
 }
 
@@ -464,6 +566,8 @@ int dpg_bound_aggregate(dpg_ctx *ctx, const int64_t *pid, const int64_t *pk, con
                 : (p->max_partitions_contributed <= 0 || p->max_contributions_per_partition <= 0))
         return fail(ctx, DPG_ERR_INVALID_ARG, "contribution bounds must be positive");
     if (n >= 0xFFFFFFFFll) return fail(ctx, DPG_ERR_UNSUPPORTED, "n must be < 2^32 per device");
+    if (p->pid_count < 0 || p->pid_count > (1ll << 32))
+        return fail(ctx, DPG_ERR_INVALID_ARG, "pid_count must be in [0, 2^32]");
     const bool var = (p->metric_mask & (DPG_M_MEAN | DPG_M_VARIANCE)) != 0;
     const bool need_values = (p->metric_mask & (DPG_M_SUM | DPG_M_MEAN | DPG_M_VARIANCE)) != 0;
     if (need_values && n > 0 && !value)
@@ -494,63 +598,42 @@ int dpg_bound_aggregate(dpg_ctx *ctx, const int64_t *pid, const int64_t *pk, con
         h.n_scalar = n;
         HIP_TRY(hipMemcpyAsync(&ctl->n_scalar, &h.n_scalar, 8, hipMemcpyHostToDevice, s));
     }
-    WS(recA, Rec16, "recA", n);
-    WS(recB, Rec16, "recB", n);
-
-    // ---- level plan: total hash bits so buckets average ~kBucketTarget
-    const uint32_t target = ctx->bucket_target
-                                ? ctx->bucket_target
-                                : std::min<uint32_t>(ctx->bucket_cap, var ? kCap32 : kCap16) / 2;
-    uint32_t bits_total = std::max<uint32_t>(1, ceil_log2((double)n / std::max<uint32_t>(1, target)));
-    int levels = (int)((bits_total + 9) / 10);
-    if (levels > kMaxLevels) levels = kMaxLevels, bits_total = 10 * kMaxLevels;
-    uint32_t lbits[kMaxLevels] = {0, 0, 0};
-    for (int l = 0; l < levels; ++l) lbits[l] = bits_total / levels + (l < (int)(bits_total % levels));
-
-    Rec16 *cur = nullptr;
-    int64_t *bstart = nullptr;
-    uint32_t *bcnt = nullptr;
-    uint32_t S = 1;
-    uint32_t shift = 32;
-    for (int l = 0; l < levels; ++l) {
-        const uint32_t F = 1u << lbits[l];
-        shift -= lbits[l];
-        DigPid dig{shift, F - 1};
-        Rec16 *dst = (l % 2 == 0) ? recA : recB;
-        char tag[16];
-        std::snprintf(tag, sizeof(tag), "lvl%d", l);
-        stage(ctx, s, l == 0 ? "partition1" : (l == 1 ? "partition2" : "partition3"));
-        int r;
-        if (l == 0) {
-            SrcSoA src{pid, pk, need_values ? value : nullptr, p->public_mask, P, &ctl->err};
-            r = run_level<SrcSoA, Rec16, DigPid, kItemsPerThread>(
-                ctx, s, src, dig, 1u, nullptr, nullptr, &ctl->n_scalar, n, F, lbits[l], dst, tag,
-                &bstart, &bcnt, &ctl->ntiles[l]);
-        } else {
-            r = run_level<SrcAoS<Rec16>, Rec16, DigPid, kItemsPerThread>(
-                ctx, s, SrcAoS<Rec16>{cur}, dig, S, bstart, bcnt, nullptr, n, F, lbits[l], dst,
-                tag, &bstart, &bcnt, &ctl->ntiles[l]);
-        }
-        if (r) return r;
-        cur = dst;
-        S *= F;
+    // ---- privacy-id range
+    int64_t pid_min = p->pid_min;
+    uint64_t U = (uint64_t)p->pid_count;
+    if (U == 0) {
+        stage(ctx, s, "pidrange");
+        const unsigned long long init[2] = {~0ull, 0ull};
+        HIP_TRY(hipMemcpyAsync(&ctl->pid_lo, init, 16, hipMemcpyHostToDevice, s));
+        const int64_t blocks = std::min<int64_t>((n + 255) / 256, (int64_t)ctx->n_cu * 8);
+        k_pid_minmax<<<(unsigned)blocks, 256, 0, s>>>(pid, n, &ctl->pid_lo, &ctl->pid_hi);
+        LAUNCH_CHECK();
+        unsigned long long h[2];
+        HIP_TRY(hipMemcpyAsync(h, &ctl->pid_lo, 16, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        const int64_t lo = (int64_t)(h[0] ^ 0x8000000000000000ull);
+        const int64_t hi = (int64_t)(h[1] ^ 0x8000000000000000ull);
+        const uint64_t span = (uint64_t)hi - (uint64_t)lo;
+        if (span >= (1ull << 32))
+            return fail(ctx, DPG_ERR_KEY_RANGE, "privacy ids span more than 2^32 values");
+        pid_min = lo;
+        U = span + 1;
     }
-    const uint32_t B = S;
-    BoundParams bp = to_bound(p, ctx->seed);
-    bp.err = &ctl->err;
-    bp.progress = nullptr;
-    bp.phase_cyc = nullptr;
-    Rec16 *other = (cur == recA) ? recB : recA;
-    if (!var) {
-        Item16 *items = reinterpret_cast<Item16 *>(other);
-        Item16 *items2 = reinterpret_cast<Item16 *>(cur);
-        return bound_and_reduce<Item16>(ctx, s, cur, bstart, bcnt, B, shift, bp, items, items2, n, P, out,
-                                         ctl);
-    }
-    WS(it32a, Item32, "items32a", n);
-    WS(it32b, Item32, "items32b", n);
-    return bound_and_reduce<Item32>(ctx, s, cur, bstart, bcnt, B, shift, bp, it32a, it32b, n, P, out,
-                                     ctl);
+    // ---- level plan: hash bits so that fine buckets average ~target records
+    Plan pl;
+    pl.P = P;
+    pl.kbits = std::max<uint32_t>(1, bits_for(U));
+    pl.pkbits = std::max<uint32_t>(1, bits_for((uint64_t)P));
+    const uint32_t target = ctx->bucket_target ? ctx->bucket_target : kBucketTarget;
+    uint32_t bits_total = bits_for((uint64_t)((n + target - 1) / target));
+    bits_total = std::max<uint32_t>(1, std::min<uint32_t>(bits_total, kMaxB1 + kMaxB2));
+    bits_total = std::min<uint32_t>(bits_total, pl.kbits);
+    pl.b1 = std::min<uint32_t>(kMaxB1, bits_total);
+    pl.b2 = bits_total - pl.b1;
+    const uint32_t ib = std::max<uint32_t>(1, bits_for((uint64_t)n));
+    const bool r8 = (pl.kbits - pl.b1) + pl.pkbits + ib <= 64;
+    if (r8) return pipeline<R8>(ctx, s, pid, pk, value, n, p, out, ctl, pl, pid_min, U, ib);
+    return pipeline<R16>(ctx, s, pid, pk, value, n, p, out, ctl, pl, pid_min, U, ib);
 }
 
 int dpg_select_and_noise(dpg_ctx *ctx, const dpg_partials *in, const dpg_select_params *sel,

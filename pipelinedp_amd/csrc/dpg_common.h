@@ -1,9 +1,10 @@
 // dpg_common.h -- device helpers shared by the gfx950 kernels of libdpg.
 //
-// Keyed counter-based randomness (Philox4x32-10) and the granular noise
-// samplers.  The same definitions are restated on the CPU in
-// oracle/dp_oracle.c; GPU and oracle must agree bit for bit on every
-// priority and selection uniform, and to within one granule on noise.
+// Keyed counter-based randomness (Philox4x32-10), the granular noise
+// samplers, the privacy-id hash and the bucketed record formats.  The same
+// definitions are restated on the CPU in oracle/dp_oracle.c; GPU and oracle
+// must agree bit for bit on every priority and selection uniform, and to
+// within one granule on noise.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -15,10 +16,55 @@
 
 namespace dpg {
 
-struct alignas(16) Rec16 {  // one bucketed record (AoS, one dwordx4)
-    uint32_t pid;
-    uint32_t pk;
-    double v;
+// ------------------------------------------------------------ record formats
+// A bucketed record carries a key and the record's index in the caller's
+// input (values are gathered by index, only for records that survive
+// bounding).  key = (h << pkbits) | pk with h = hk(pid - pid_min) on kbits
+// bits; the stored key drops the level-1 digit (the top b1 bits of h), which
+// the bucket position implies.
+//   R8 : one word, stored_key << ib | idx    (when it fits 64 bits)
+//   R16: stored_key, idx                      (always fits)
+struct alignas(8) R8 {
+    uint64_t w;
+};
+struct alignas(16) R16 {
+    uint64_t key;
+    uint32_t idx;
+    uint32_t pad;
+};
+
+struct Fmt {
+    uint32_t ib;      // R8: bits of the record index
+    uint32_t pkbits;  // bits of the partition key
+    uint32_t kbits;   // bits of the privacy-id hash
+    uint32_t b1;      // level-1 digit bits (dropped from the stored key)
+};
+
+template <class R>
+struct RecOps;
+template <>
+struct RecOps<R8> {
+    static __host__ __device__ __forceinline__ uint64_t key(const R8 &r, const Fmt &f) {
+        return r.w >> f.ib;
+    }
+    static __host__ __device__ __forceinline__ uint32_t idx(const R8 &r, const Fmt &f) {
+        return (uint32_t)(r.w & ((1ull << f.ib) - 1ull));
+    }
+    static __host__ __device__ __forceinline__ R8 make(uint64_t key, uint32_t idx, const Fmt &f) {
+        return R8{(key << f.ib) | idx};
+    }
+};
+template <>
+struct RecOps<R16> {
+    static __host__ __device__ __forceinline__ uint64_t key(const R16 &r, const Fmt &) {
+        return r.key;
+    }
+    static __host__ __device__ __forceinline__ uint32_t idx(const R16 &r, const Fmt &) {
+        return r.idx;
+    }
+    static __host__ __device__ __forceinline__ R16 make(uint64_t key, uint32_t idx, const Fmt &) {
+        return R16{key, idx, 0u};
+    }
 };
 
 struct alignas(16) Item16 {  // one kept (pid, pk) pair: COUNT / SUM / PID
@@ -35,6 +81,59 @@ struct alignas(16) Item32 {  // one kept pair with MEAN / VARIANCE moments
     double nsq;
 };
 
+// ------------------------------------------------------------ privacy-id hash
+// A bijection on [0, 2^bits): xorshift / odd-multiply rounds (the Murmur3
+// finaliser's shape, shifts scaled to the width).  The top bits pick the
+// bucket; the bound kernels invert it to recover the privacy id.
+struct HashK {
+    uint32_t bits, mask, s1, s2, s3, m1, m2, i1, i2;
+};
+
+__host__ __device__ __forceinline__ uint32_t hk(uint32_t x, const HashK &H) {
+    x &= H.mask;
+    x ^= x >> H.s1;
+    x = (x * H.m1) & H.mask;
+    x ^= x >> H.s2;
+    x = (x * H.m2) & H.mask;
+    x ^= x >> H.s3;
+    return x;
+}
+
+__host__ __device__ __forceinline__ uint32_t unxorshift(uint32_t y, uint32_t s, uint32_t bits) {
+    uint32_t x = y;
+    for (uint32_t k = s; k < bits; k += s) x = y ^ (x >> s);
+    return x;
+}
+
+__host__ __device__ __forceinline__ uint32_t hk_inv(uint32_t y, const HashK &H) {
+    uint32_t x = unxorshift(y & H.mask, H.s3, H.bits);
+    x = (x * H.i2) & H.mask;
+    x = unxorshift(x, H.s2, H.bits);
+    x = (x * H.i1) & H.mask;
+    return unxorshift(x, H.s1, H.bits);
+}
+
+inline uint32_t inv_odd32(uint32_t m) {
+    uint32_t x = m;  // Newton: x <- x (2 - m x), 5 steps reach 32 bits
+    for (int k = 0; k < 5; ++k) x *= 2u - m * x;
+    return x;
+}
+
+inline HashK make_hash(uint32_t bits) {
+    HashK H;
+    H.bits = bits;
+    H.mask = bits >= 32 ? 0xFFFFFFFFu : ((1u << bits) - 1u);
+    H.s1 = (bits + 1) / 2;
+    H.s2 = (bits * 13) / 32 > 0 ? (bits * 13) / 32 : 1;
+    H.s3 = (bits + 1) / 2;
+    H.m1 = 0x85EBCA6Bu;
+    H.m2 = 0xC2B2AE35u;
+    H.i1 = inv_odd32(H.m1);
+    H.i2 = inv_odd32(H.m2);
+    return H;
+}
+
+// ------------------------------------------------------------------ Philox
 __host__ __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0,
                                                        uint32_t k1) {
 #pragma unroll
@@ -55,8 +154,7 @@ __host__ __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k
     }
 }
 
-// Murmur3 finaliser: a bijection on 32-bit ints; its top bits pick the
-// privacy-id bucket.
+// Murmur3 finaliser (hash-table slots).
 __host__ __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
     h ^= h >> 16;
     h *= 0x85EBCA6Bu;
@@ -66,16 +164,19 @@ __host__ __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
     return h;
 }
 
-__device__ __forceinline__ uint32_t pair_prio(uint64_t seed, uint32_t pid, uint32_t pk) {
-    uint32_t c[4] = {pid, pk, 0u, 0u};
+// Pair priority: philox(seed ^ TAG_PAIR; pid, pk) -- the mpc sampler key.
+__device__ __forceinline__ uint32_t pair_prio(uint64_t seed, uint64_t pid, uint32_t pk) {
+    uint32_t c[4] = {(uint32_t)pid, pk, (uint32_t)(pid >> 32), 0u};
     philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32) ^ DPG_TAG_PAIR);
     return c[0];
 }
 
-__device__ __forceinline__ uint64_t rec_prio(uint64_t seed, uint32_t pid, uint32_t pk,
-                                             uint64_t vbits, uint32_t occ) {
-    uint32_t c[4] = {pid, pk, (uint32_t)vbits, (uint32_t)(vbits >> 32)};
-    philox4x32_10(c, (uint32_t)seed ^ (occ * 0x9E3779B9u),
+// Record priority: philox(seed ^ TAG_REC; pid, pk, global record id) -- the
+// mcpp / L1 sampler key.
+__device__ __forceinline__ uint64_t rec_prio(uint64_t seed, uint64_t pid, uint32_t pk,
+                                             uint64_t gidx) {
+    uint32_t c[4] = {(uint32_t)pid, pk, (uint32_t)gidx, (uint32_t)(gidx >> 32)};
+    philox4x32_10(c, (uint32_t)seed ^ ((uint32_t)(pid >> 32) * 0x9E3779B9u),
                   (uint32_t)(seed >> 32) ^ DPG_TAG_REC);
     return ((uint64_t)c[0] << 32) | c[1];
 }
@@ -126,8 +227,6 @@ __device__ __forceinline__ void select_uniforms(uint64_t seed, uint64_t pk, uint
 __device__ __forceinline__ double clampd(double x, double lo, double hi) {
     return x < lo ? lo : (x > hi ? hi : x);
 }
-
-__device__ __forceinline__ int lane_id() { return __lane_id(); }
 
 // Wave-level exclusive prefix of a per-lane count; returns the wave total.
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, uint32_t &total) {

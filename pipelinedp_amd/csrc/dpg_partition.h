@@ -2,22 +2,26 @@
 // (and of kept pairs by partition-key range) for gfx950.
 //
 // One level = hist -> scan -> digit-base -> scatter.  A level splits every
-// segment of its input into F <= 1024 digit buckets.  The scatter stages a
-// sub-tile of 8192 records through LDS, ranked per digit with wave-
-// aggregated LDS atomics, so each digit leaves as one contiguous run per
-// sub-tile (8 records = 128 B per digit on average at F = 1024): coalesced
+// segment of its input into F <= 2048 digit buckets.  The scatter stages a
+// sub-tile of records through LDS, ranked per digit with wave-aggregated LDS
+// atomics, so each digit leaves as one contiguous run per sub-tile: coalesced
 // writes without per-record global atomics.  Order inside a digit is not
-// preserved (nothing downstream depends on it: the sampler keys on record
-// contents, see DESIGN.md "Randomness").
+// preserved (nothing downstream depends on it: the samplers key on the
+// global record id, see DESIGN.md "Randomness").
+//
+// Sources expose fetch(i) -> Raw (the global loads, issued one sub-tile ahead)
+// and decode(Raw, i, rec, digit) -> keep; sources whose records still carry
+// their digit recompute it at write-out, the level-1 source (whose records
+// drop the level-1 digit) stages it in LDS beside the record.
 #pragma once
 
 #include "dpg_common.h"
 
 namespace dpg {
 
-constexpr int kPartThreads = 1024;          // 16 waves
-constexpr int kItemsPerThread = 8;          // 8192 records per sub-tile
-constexpr int kSubTile = kPartThreads * kItemsPerThread;
+constexpr int kPartThreads = 1024;  // 16 waves
+
+__host__ __device__ constexpr size_t a16(size_t x) { return (x + 15) & ~(size_t)15; }
 
 struct TileDesc {
     int64_t begin, end;
@@ -26,61 +30,69 @@ struct TileDesc {
 };
 
 // ---------------------------------------------------------------- sources
-// Level 1: the caller's structure-of-arrays input (int64 pid, int64 pk,
-// double value) -> Rec16.  Drops records of non-public partitions.  Keys
-// outside the supported range raise err bit 1 (the call then fails); such a
-// record is still kept, so the scatter agrees with the histogram, which only
-// reads pid (and pk when there is a public-partition filter).
-struct SrcSoA {
-    static constexpr bool kPlainFetch = false;
+// Level 1: the caller's int64 pid / pk columns -> R (key residual, index).
+// Drops records of non-public partitions.  Keys outside the declared ranges
+// raise err bit 1 (the call then fails before any bucket is bounded); such a
+// record is still kept so that the scatter agrees with the histogram.
+template <class R>
+struct SrcSoAKey {
+    static constexpr bool kDigitFromRec = false;
+    struct Raw {
+        int64_t pid, pk;
+    };
     const int64_t *pid;
     const int64_t *pk;
-    const double *v;
     const uint8_t *pub;  // public-partition bitmap or null
     int64_t P;
+    int64_t pid_min;
+    uint64_t U;          // privacy ids in [pid_min, pid_min + U)
+    HashK H;
+    Fmt f;
+    uint64_t kmask;      // stored key bits
+    uint32_t dshift;     // kbits - b1
     uint32_t *err;
-    __device__ __forceinline__ bool load(int64_t i, Rec16 &r) const {
-        const int64_t a = pid[i], b = pk[i];
-        r.v = v ? v[i] : 0.0;
-        r.pid = (uint32_t)a;
-        r.pk = (uint32_t)b;
-        const bool in_range = (uint64_t)a < 0xFFFFFFFFull && (uint64_t)b < (uint64_t)P;
+    __device__ __forceinline__ Raw fetch(int64_t i) const { return Raw{pid[i], pk[i]}; }
+    __device__ __forceinline__ bool decode(const Raw &x, int64_t i, R &r, uint32_t &d) const {
+        const uint64_t a = (uint64_t)(x.pid - pid_min);
+        const bool in_range = a < U && (uint64_t)x.pk < (uint64_t)P;
         if (!in_range) atomicOr(err, 1u);
-        return !(pub && in_range && !((pub[b >> 3] >> (b & 7)) & 1));
+        const uint32_t h = hk((uint32_t)a, H);
+        d = h >> dshift;
+        const uint64_t key = (((uint64_t)h << f.pkbits) | (uint64_t)x.pk) & kmask;
+        r = RecOps<R>::make(key, (uint32_t)i, f);
+        return !(pub && in_range && !((pub[x.pk >> 3] >> (x.pk & 7)) & 1));
     }
-};
-
-// The level-1 histogram's view of SrcSoA: the same keep decision, reading
-// only what it needs.
-struct SrcSoAHist {
-    const int64_t *pid;
-    const int64_t *pk;
-    const uint8_t *pub;
-    int64_t P;
-    __device__ __forceinline__ bool load(int64_t i, Rec16 &r) const {
-        const int64_t a = pid[i];
-        r.pid = (uint32_t)a;
+    // histogram view: the same digit and keep decision from pid (and pk
+    // only when a public-partition filter applies)
+    __device__ __forceinline__ bool hist(int64_t i, uint32_t &d) const {
+        const uint64_t a = (uint64_t)(pid[i] - pid_min);
+        d = hk((uint32_t)a, H) >> dshift;
         if (!pub) return true;
         const int64_t b = pk[i];
-        const bool in_range = (uint64_t)a < 0xFFFFFFFFull && (uint64_t)b < (uint64_t)P;
+        const bool in_range = a < U && (uint64_t)b < (uint64_t)P;
         return !(in_range && !((pub[b >> 3] >> (b & 7)) & 1));
     }
 };
 
-template <class Src>
-__host__ __device__ inline Src hist_view(const Src &s) {
-    return s;
-}
-__host__ __device__ inline SrcSoAHist hist_view(const SrcSoA &s) {
-    return SrcSoAHist{s.pid, s.pk, s.pub, s.P};
-}
-
-template <class T>
+// Bucketed records; digit = bits [shift, shift + log2 F) of the stored key.
+template <class R>
 struct SrcAoS {
-    static constexpr bool kPlainFetch = true;
-    const T *a;
-    __device__ __forceinline__ bool load(int64_t i, T &r) const {
-        r = a[i];
+    static constexpr bool kDigitFromRec = true;
+    using Raw = R;
+    const R *a;
+    Fmt f;
+    uint32_t shift, mask;
+    __device__ __forceinline__ R fetch(int64_t i) const { return a[i]; }
+    __device__ __forceinline__ uint32_t digit(const R &r) const {
+        return (uint32_t)(RecOps<R>::key(r, f) >> shift) & mask;
+    }
+    __device__ __forceinline__ bool decode(const R &x, int64_t, R &r, uint32_t &d) const {
+        r = x;
+        d = digit(x);
+        return true;
+    }
+    __device__ __forceinline__ bool hist(int64_t i, uint32_t &d) const {
+        d = digit(a[i]);
         return true;
     }
 };
@@ -88,16 +100,19 @@ struct SrcAoS {
 // Items of S per-workgroup regions read as one sequence: element i lives in
 // region s with pre[s] <= i < pre[s + 1], at a[off[s] + i - pre[s]].  Each
 // thread walks increasing i, so the region found last is cached in
-// registers and the binary search runs only when i leaves it.
+// registers and the binary search runs only when i leaves it.  Digit =
+// pk >> shift (partition-key ranges).
 template <class T>
 struct SrcSeg {
-    static constexpr bool kPlainFetch = false;
+    static constexpr bool kDigitFromRec = true;
+    using Raw = T;
     const T *a;
     const int64_t *pre;  // [S + 1]
     const int64_t *off;  // [S]
     uint32_t S;
+    uint32_t shift;
     int64_t lo = 0, hi = 0, base = 0;  // cached region [lo, hi), a index = base + i
-    __device__ __forceinline__ bool load(int64_t i, T &r) {
+    __device__ __forceinline__ T fetch(int64_t i) {
         if (i < lo || i >= hi) {
             uint32_t l = 0, h = S;
             while (h - l > 1) {
@@ -109,23 +124,18 @@ struct SrcSeg {
             hi = pre[l + 1];
             base = off[l] - lo;
         }
-        r = a[base + i];
+        return a[base + i];
+    }
+    __device__ __forceinline__ uint32_t digit(const T &r) const { return r.pk >> shift; }
+    __device__ __forceinline__ bool decode(const T &x, int64_t, T &r, uint32_t &d) const {
+        r = x;
+        d = digit(x);
         return true;
     }
-};
-
-// ----------------------------------------------------------------- digits
-struct DigPid {
-    uint32_t shift, mask;
-    __device__ __forceinline__ uint32_t operator()(const Rec16 &r) const {
-        return (fmix32(r.pid) >> shift) & mask;
+    __device__ __forceinline__ bool hist(int64_t i, uint32_t &d) {
+        d = digit(fetch(i));
+        return true;
     }
-};
-
-template <class T>
-struct DigPk {
-    uint32_t shift;
-    __device__ __forceinline__ uint32_t operator()(const T &r) const { return r.pk >> shift; }
 };
 
 // ------------------------------------------------------------ tile table
@@ -153,8 +163,8 @@ __global__ void k_build_tiles(const int64_t *seg_start, const uint32_t *seg_cnt,
 }
 
 // ---------------------------------------------------------------- hist
-template <class Src, class Rec, class Dig>
-__global__ __launch_bounds__(kPartThreads) void k_hist(Src src_in, Dig dig, const TileDesc *tiles,
+template <class Src>
+__global__ __launch_bounds__(kPartThreads) void k_hist(Src src_in, const TileDesc *tiles,
                                                        const uint32_t *ntiles, uint32_t F,
                                                        uint32_t *hist) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lh[];  // [4][F]
@@ -169,17 +179,17 @@ __global__ __launch_bounds__(kPartThreads) void k_hist(Src src_in, Dig dig, cons
     Src src = src_in;  // per-thread copy (sources may cache lookup state)
     int64_t i = td.begin + tid;
     for (; i + 3 * kPartThreads < td.end; i += 4 * kPartThreads) {
-        Rec r[4];
+        uint32_t d[4];
         bool ok[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) ok[u] = src.load(i + u * kPartThreads, r[u]);
+        for (int u = 0; u < 4; ++u) ok[u] = src.hist(i + u * kPartThreads, d[u]);
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-            if (ok[u]) atomicAdd(&my[dig(r[u])], 1u);
+            if (ok[u]) atomicAdd(&my[d[u]], 1u);
     }
     for (; i < td.end; i += kPartThreads) {
-        Rec r;
-        if (src.load(i, r)) atomicAdd(&my[dig(r)], 1u);
+        uint32_t d;
+        if (src.hist(i, d)) atomicAdd(&my[d], 1u);
     }
     __syncthreads();
     for (uint32_t d = tid; d < F; d += kPartThreads)
@@ -241,19 +251,35 @@ __device__ __forceinline__ uint32_t block_excl_scan_1024(uint32_t x, uint32_t *s
     return e + pre;
 }
 
-// grid S: base[s][d] = seg_start[s] + exclusive_prefix_d(tot[s][.])
+// Exclusive scan of cnt[0, F) (F <= 2048) into dstart by 1024 threads
+// (two consecutive digits per thread); returns the total.  Ends with a
+// barrier: every dstart entry is visible to every thread on return.
+__device__ __forceinline__ uint32_t block_scan_digits(const uint32_t *cnt, uint32_t *dstart,
+                                                      uint32_t F, uint32_t *sh16) {
+    const uint32_t d0 = 2 * threadIdx.x;
+    const uint32_t c0 = d0 < F ? cnt[d0] : 0u;
+    const uint32_t c1 = d0 + 1 < F ? cnt[d0 + 1] : 0u;
+    uint32_t total;
+    const uint32_t e = block_excl_scan_1024(c0 + c1, sh16, total);
+    if (d0 < F) dstart[d0] = e;
+    if (d0 + 1 < F) dstart[d0 + 1] = e + c0;
+    __syncthreads();
+    return total;
+}
+
+// grid S: base[s][d] = seg_start[s] + exclusive_prefix_d(tot[s][.])  (F <= 2048)
 __global__ __launch_bounds__(1024) void k_digit_base(const int64_t *seg_start, uint32_t F,
-                                                     const uint32_t *tot, int64_t *base,
-                                                     int64_t *seg_total_out) {
+                                                     const uint32_t *tot, int64_t *base) {
     __shared__ uint32_t sh[16];
     const uint32_t s = blockIdx.x;
-    const uint32_t d = threadIdx.x;
-    uint32_t x = d < F ? tot[(size_t)s * F + d] : 0u;
+    const uint32_t d0 = 2 * threadIdx.x;
+    const uint32_t c0 = d0 < F ? tot[(size_t)s * F + d0] : 0u;
+    const uint32_t c1 = d0 + 1 < F ? tot[(size_t)s * F + d0 + 1] : 0u;
     uint32_t total;
-    uint32_t e = block_excl_scan_1024(x, sh, total);
-    int64_t st = seg_start ? seg_start[s] : 0;
-    if (d < F) base[(size_t)s * F + d] = st + e;
-    if (d == 0 && seg_total_out) seg_total_out[s] = total;
+    const uint32_t e = block_excl_scan_1024(c0 + c1, sh, total);
+    const int64_t st = seg_start ? seg_start[s] : 0;
+    if (d0 < F) base[(size_t)s * F + d0] = st + e;
+    if (d0 + 1 < F) base[(size_t)s * F + d0 + 1] = st + e + c0;
 }
 
 // ---------------------------------------------------------------- scatter
@@ -276,40 +302,55 @@ __device__ __forceinline__ uint32_t wave_agg_rank(uint32_t *cnt, uint32_t d, boo
     return basev + below;
 }
 
-// Records travel through registers and LDS as raw 16-byte words (struct
-// copies of Rec would be demoted to scratch by the compiler).
-template <class Rec>
+// Records travel through registers and LDS as raw 8- or 16-byte words
+// (struct copies would be demoted to scratch by the compiler).
+template <class T, bool kQuad = (sizeof(T) % 16 == 0)>
 struct Words {
-    static constexpr int N = sizeof(Rec) / 16;
+    static constexpr int N = sizeof(T) / 16;
     uint4 w[N];
 };
-template <class Rec>
-__device__ __forceinline__ Words<Rec> to_words(const Rec &r) {
-    Words<Rec> x;
-    __builtin_memcpy(&x, &r, sizeof(Rec));
+template <class T>
+struct Words<T, false> {
+    static constexpr int N = sizeof(T) / 8;
+    uint2 w[N];
+};
+template <class T>
+__device__ __forceinline__ Words<T> to_words(const T &r) {
+    Words<T> x;
+    __builtin_memcpy(&x, &r, sizeof(T));
     return x;
 }
-template <class Rec>
-__device__ __forceinline__ Rec from_words(const Words<Rec> &x) {
-    Rec r;
-    __builtin_memcpy(&r, &x, sizeof(Rec));
+template <class T>
+__device__ __forceinline__ T from_words(const Words<T> &x) {
+    T r;
+    __builtin_memcpy(&r, &x, sizeof(T));
     return r;
 }
 
-template <class Src, class Rec, class Dig, int IPT>
-__global__ __launch_bounds__(kPartThreads) void k_scatter(Src src_in, Dig dig, const TileDesc *tiles,
+// LDS bytes of one k_scatter instantiation.
+template <class Src, class Rec, int IPT, int FMAX>
+constexpr size_t scatter_lds() {
+    return (size_t)sizeof(Rec) * kPartThreads * IPT +
+           (Src::kDigitFromRec ? 0 : a16((size_t)2 * kPartThreads * IPT)) + (size_t)FMAX * 12 +
+           64;
+}
+
+template <class Src, class Rec, int IPT, int FMAX>
+__global__ __launch_bounds__(kPartThreads) void k_scatter(Src src_in, const TileDesc *tiles,
                                                           const uint32_t *ntiles, uint32_t F,
                                                           uint32_t bits, const uint32_t *off,
                                                           const int64_t *base, Rec *out) {
-    constexpr int sub_items = IPT;
-    // LDS: staging Rec[sub], cnt[F], dstart[F], cur int64[F], sh16
+    constexpr int SUB = kPartThreads * IPT;
+    constexpr bool kSD = !Src::kDigitFromRec;
+    using W = Words<Rec>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    Words<Rec> *stage = reinterpret_cast<Words<Rec> *>(smem);
-    const int sub = kPartThreads * sub_items;
-    uint32_t *cnt = reinterpret_cast<uint32_t *>(smem + sizeof(Rec) * sub);
-    uint32_t *dstart = cnt + 1024;
-    int64_t *cur = reinterpret_cast<int64_t *>(dstart + 1024);
-    uint32_t *sh16 = reinterpret_cast<uint32_t *>(cur + 1024);
+    W *stage = reinterpret_cast<W *>(smem);
+    uint16_t *sdig = reinterpret_cast<uint16_t *>(smem + sizeof(Rec) * SUB);
+    const size_t o = sizeof(Rec) * SUB + (kSD ? a16((size_t)2 * SUB) : 0);
+    uint32_t *cnt = reinterpret_cast<uint32_t *>(smem + o);
+    uint32_t *dstart = cnt + FMAX;
+    uint32_t *cur = dstart + FMAX;  // output positions (n < 2^32 per device)
+    uint32_t *sh16 = cur + FMAX;
 
     const uint32_t t = blockIdx.x;
     if (t >= *ntiles) return;
@@ -317,93 +358,64 @@ __global__ __launch_bounds__(kPartThreads) void k_scatter(Src src_in, Dig dig, c
     const int tid = threadIdx.x;
     Src src = src_in;  // per-thread copy (sources may cache lookup state)
     for (uint32_t d = tid; d < F; d += kPartThreads) {
-        cur[d] = base[(size_t)td.seg * F + d] + off[(size_t)t * F + d];
+        cur[d] = (uint32_t)(base[(size_t)td.seg * F + d] + off[(size_t)t * F + d]);
         cnt[d] = 0;
     }
-    __syncthreads();
-    if constexpr (Src::kPlainFetch) {
-        // Software pipeline: the records of sub-tile j + 1 are fetched into
-        // the (then dead) registers right after sub-tile j is staged in LDS,
-        // so the loads are in flight during j's write-out.
-        Words<Rec> r[IPT];
-        bool inb[IPT];
-#pragma unroll
-        for (int j = 0; j < IPT; ++j) {
-            const int64_t i = td.begin + (int64_t)j * kPartThreads + tid;
-            inb[j] = i < td.end;
-            if (inb[j]) r[j] = to_words(src.a[i]);
-        }
-        for (int64_t sb = td.begin; sb < td.end; sb += sub) {
-            uint32_t dg[IPT], rk[IPT];
-#pragma unroll
-            for (int j = 0; j < IPT; ++j) dg[j] = inb[j] ? dig(from_words<Rec>(r[j])) : 0u;
-#pragma unroll
-            for (int j = 0; j < IPT; ++j) rk[j] = wave_agg_rank(cnt, dg[j], inb[j], bits);
-            __syncthreads();
-            uint32_t c = tid < (int)F ? cnt[tid] : 0u;
-            uint32_t total;
-            uint32_t e = block_excl_scan_1024(c, sh16, total);
-            if (tid < (int)F) dstart[tid] = e;
-            __syncthreads();
-#pragma unroll
-            for (int j = 0; j < IPT; ++j)
-                if (inb[j]) stage[dstart[dg[j]] + rk[j]] = r[j];
-            __syncthreads();
-            const int64_t nb = sb + sub;
-#pragma unroll
-            for (int j = 0; j < IPT; ++j) {
-                const int64_t i = nb + (int64_t)j * kPartThreads + tid;
-                inb[j] = i < td.end;
-                if (inb[j]) r[j] = to_words(src.a[i]);
-            }
-            for (uint32_t k = tid; k < total; k += kPartThreads) {
-                Words<Rec> x = stage[k];
-                uint32_t dd = dig(from_words<Rec>(x));
-                *reinterpret_cast<Words<Rec> *>(&out[cur[dd] + (int64_t)(k - dstart[dd])]) = x;
-            }
-            __syncthreads();
-            if (tid < (int)F) {
-                cur[tid] += cnt[tid];
-                cnt[tid] = 0;
-            }
-            __syncthreads();
-        }
-        return;
-    }
-    for (int64_t sb = td.begin; sb < td.end; sb += sub) {
-        Words<Rec> r[IPT];
-        uint32_t dg[IPT];
-        uint32_t rk[IPT];
-        bool ok[IPT];
-#pragma unroll
-        for (int j = 0; j < IPT; ++j) {
-            int64_t i = sb + (int64_t)j * kPartThreads + tid;
-            Rec x;
-            ok[j] = i < td.end && src.load(i, x);
-            dg[j] = ok[j] ? dig(x) : 0u;
-            r[j] = to_words(x);
-        }
-#pragma unroll
-        for (int j = 0; j < IPT; ++j) rk[j] = wave_agg_rank(cnt, dg[j], ok[j], bits);
-        __syncthreads();
-        uint32_t c = tid < (int)F ? cnt[tid] : 0u;
-        uint32_t total;
-        uint32_t e = block_excl_scan_1024(c, sh16, total);
-        if (tid < (int)F) dstart[tid] = e;
-        __syncthreads();
+    // software pipeline: the raw loads of sub-tile j + 1 are issued right
+    // after sub-tile j is staged in LDS, so they are in flight during j's
+    // write-out
+    // Loads are unconditional with the index clamped into the sub-tile (a
+    // guarded load becomes a branch with its own vmcnt(0) wait, serialising
+    // the sub-tile's loads); lanes past the end re-read the last record.
+    typename Src::Raw raw[IPT];
+    {
+        const uint32_t lim = (uint32_t)min<int64_t>(SUB, td.end - td.begin);
 #pragma unroll
         for (int j = 0; j < IPT; ++j)
-            if (ok[j]) stage[dstart[dg[j]] + rk[j]] = r[j];
-        __syncthreads();
-        for (uint32_t k = tid; k < total; k += kPartThreads) {
-            Words<Rec> x = stage[k];
-            uint32_t dd = dig(from_words<Rec>(x));
-            *reinterpret_cast<Words<Rec> *>(&out[cur[dd] + (int64_t)(k - dstart[dd])]) = x;
+            raw[j] = src.fetch(td.begin + min((uint32_t)(j * kPartThreads + tid), lim - 1));
+    }
+    __syncthreads();
+    for (int64_t sb = td.begin; sb < td.end; sb += SUB) {
+        const uint32_t lim = (uint32_t)min<int64_t>(SUB, td.end - sb);  // uniform
+        Rec rec[IPT];
+        uint32_t dr[IPT];  // digit | rank << 12, or ~0 for a dropped record
+#pragma unroll
+        for (int j = 0; j < IPT; ++j) {
+            const uint32_t o = j * kPartThreads + tid;
+            uint32_t d = 0;
+            const bool ok = o < lim && src.decode(raw[j], sb + o, rec[j], d);
+            const uint32_t rk = wave_agg_rank(cnt, ok ? d : 0u, ok, bits);
+            dr[j] = ok ? (d | (rk << 12)) : ~0u;
         }
         __syncthreads();
-        if (tid < (int)F) {
-            cur[tid] += cnt[tid];
-            cnt[tid] = 0;
+        const uint32_t total = block_scan_digits(cnt, dstart, F, sh16);
+#pragma unroll
+        for (int j = 0; j < IPT; ++j)
+            if (dr[j] != ~0u) {
+                const uint32_t d = dr[j] & 0xFFFu;
+                const uint32_t pos = dstart[d] + (dr[j] >> 12);
+                stage[pos] = to_words(rec[j]);
+                if constexpr (kSD) sdig[pos] = (uint16_t)d;
+            }
+        __syncthreads();
+        const int64_t nb = sb + SUB;
+        const uint32_t nlim = (uint32_t)max<int64_t>(0, min<int64_t>(SUB, td.end - nb));
+        if (nlim > 0) {
+#pragma unroll
+            for (int j = 0; j < IPT; ++j)
+                raw[j] = src.fetch(nb + min((uint32_t)(j * kPartThreads + tid), nlim - 1));
+        }
+        for (uint32_t k = tid; k < total; k += kPartThreads) {
+            const W x = stage[k];
+            uint32_t dd;
+            if constexpr (kSD) dd = sdig[k];
+            else dd = src.digit(from_words<Rec>(x));
+            *reinterpret_cast<W *>(&out[(size_t)cur[dd] + (k - dstart[dd])]) = x;
+        }
+        __syncthreads();
+        for (uint32_t d = tid; d < F; d += kPartThreads) {
+            cur[d] += cnt[d];
+            cnt[d] = 0;
         }
         __syncthreads();
     }

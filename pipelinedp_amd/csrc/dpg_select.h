@@ -80,8 +80,7 @@ __global__ void k_reduce_items_direct(Src items, const uint32_t *n_items, Partia
     const uint32_t n = *n_items;
     Src src = items;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        Item it;
-        src.load(i, it);
+        const Item it = src.fetch(i);
         atomicAdd((unsigned long long *)&out.rows[it.pk], 1ull);
         atomicAdd((unsigned long long *)&out.count[it.pk], (unsigned long long)it.cnt);
         if (out.sum) atomicAdd(&out.sum[it.pk], it.sum);

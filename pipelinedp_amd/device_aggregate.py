@@ -134,6 +134,7 @@ class DeviceAggregation:
                               need_pid=not self.bounds_already_enforced)
         if self.bounds_already_enforced:
             enc.pid = torch.arange(enc.n, dtype=torch.int64, device=dev)
+            enc.pid_min, enc.pid_count = 0, max(1, enc.n)
         # noise / selection parameters are resolved now (after compute_budgets)
         noise = (self.plan.noise_fields(self.noise_enabled) if self.plan is not None else
                  dict(noise_kind=0, family=0, slot_mask=0, n_outputs=0, out_src=[0] * 8,
@@ -153,6 +154,8 @@ class DeviceAggregation:
             nsq = torch.empty(P, **f64) if var else None
             bfields = self._bound_fields(P)
             bound = _native.fill(_native.BoundParams, bfields)
+            bound.pid_min, bound.pid_count = enc.pid_min, enc.pid_count
+            bound.rec_id_offset = enc.rec_id_offset
             if enc.public_mask is not None and self.drop_non_public:
                 bound.public_mask = enc.public_mask.data_ptr()
             partials = _native.Partials(P, rows.data_ptr(), count.data_ptr(),

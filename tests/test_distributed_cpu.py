@@ -39,7 +39,8 @@ def _worker(rank, world, port, q):
     pid, pk, val = _data()
     shard = distributed.shard_of(torch.as_tensor(pid), world).numpy()
     m = shard == rank
-    part = oracle.bound_aggregate(pid[m], pk[m], val[m], FIELDS, 99)
+    # global record ids keep the record sampler identical to the whole run
+    part = oracle.bound_aggregate(pid[m], pk[m], val[m], FIELDS, 99, rec_ids=np.nonzero(m)[0])
     tens = {k: torch.as_tensor(part[k]) for k in ("rows", "count", "sum")}
     tens.update(nsum=None, nsq=None)
     out, lo, n = distributed.reduce_scatter_partials(tens, P, dist.group.WORLD)

@@ -33,17 +33,18 @@ def test_library_exports_every_symbol(built):
 def test_struct_layouts_match_c(tmp_path):
     src = tmp_path / "layout.c"
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "dpg.h"\n'
-                   'int main(){printf("%zu %zu %zu %zu %zu %zu %zu\\n",'
+                   'int main(){printf("%zu %zu %zu %zu %zu %zu %zu %zu\\n",'
                    'sizeof(dpg_bound_params), sizeof(dpg_partials), sizeof(dpg_select_params),'
                    'sizeof(dpg_noise_params), offsetof(dpg_bound_params, public_mask),'
-                   'offsetof(dpg_select_params, public_mask), offsetof(dpg_noise_params, msq_const_value));}')
+                   'offsetof(dpg_select_params, public_mask), offsetof(dpg_noise_params, msq_const_value),'
+                   'offsetof(dpg_bound_params, rec_id_offset));}')
     exe = tmp_path / "layout"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
     got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
     want = [ctypes.sizeof(_native.BoundParams), ctypes.sizeof(_native.Partials),
             ctypes.sizeof(_native.SelectParams), ctypes.sizeof(_native.NoiseParams),
             _native.BoundParams.public_mask.offset, _native.SelectParams.public_mask.offset,
-            _native.NoiseParams.msq_const_value.offset]
+            _native.NoiseParams.msq_const_value.offset, _native.BoundParams.rec_id_offset.offset]
     assert got == want
 
 
