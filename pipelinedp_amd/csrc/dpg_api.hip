@@ -4,7 +4,7 @@
 // Pipeline of dpg_bound_aggregate (DESIGN.md "Kernels"):
 //   [pid range reduction when the caller does not declare it]
 //   level 1: SoA (pid, pk) -> packed records (key residual, record index),
-//            bucketed by the top b1 <= 10 bits of hk(pid)
+//            bucketed by the top b1 <= 11 bits of hk(pid)
 //   level 2: records -> buckets by the next b2 <= 11 hash bits (~512 records)
 //   -> k_make_chunks (greedy packing of fine buckets into <= 1024-record
 //      chunks), refine level for oversize buckets -> k_bound_chunks
@@ -34,7 +34,7 @@ using namespace dpg;
 namespace {
 
 constexpr uint32_t kBucketTarget = 512;  // average records per fine bucket
-constexpr uint32_t kMaxB1 = 10, kMaxB2 = 11;
+constexpr uint32_t kMaxB1 = 11, kMaxB2 = 11;
 constexpr uint32_t kChunkGroup = 32;     // fine buckets per packing thread
 
 struct Buf {
@@ -257,6 +257,7 @@ BoundParams to_bound(const dpg_bound_params *p, uint64_t seed) {
 
 struct Plan {
     uint32_t b1, b2, kbits, pkbits;
+    uint32_t plb;  // pid hash bits left below the fine buckets (<= 10)
     int64_t P;
 };
 
@@ -275,12 +276,12 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     WS(ostart, int64_t, "over.start", B);
     WS(ocnt, uint32_t, "over.cnt", B);
     WS(od1, uint32_t, "over.d1", B);
+    WS(ohb, uint32_t, "over.hb", B);
     const uint32_t group = std::min<uint32_t>(kChunkGroup, 1u << pl.b2);
     const uint32_t ngroups = (B + group - 1) / group;
-    k_make_chunks<<<(ngroups + 255) / 256, 256, 0, s>>>(bstart, bcnt, B, group, cap, 0u, pl.b2,
-                                                         nullptr, chunks, &ctl->n_chunks, ostart,
-                                                         ocnt, od1, &ctl->n_over,
-                                                         &ctl->over_records);
+    k_make_chunks<<<(ngroups + 255) / 256, 256, 0, s>>>(
+        bstart, bcnt, B, group, cap, 0u, pl.b2, nullptr, nullptr, pl.plb, chunks,
+        &ctl->n_chunks, ostart, ocnt, od1, ohb, &ctl->n_over, &ctl->over_records);
     LAUNCH_CHECK();
     Control hctl;
     HIP_TRY(hipMemcpyAsync(&hctl, ctl, sizeof(Control), hipMemcpyDeviceToHost, s));
@@ -297,8 +298,7 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     const uint32_t *g_d1 = od1;
     uint32_t n_global = 0;
     if (hctl.n_over > 0) {
-        const uint32_t left = pl.kbits - pl.b1 - pl.b2;  // hash bits not yet used
-        const uint32_t rbits = std::min<uint32_t>(kMaxB2, left);
+        const uint32_t rbits = std::min<uint32_t>(kMaxB2, pl.plb);  // hash bits not yet used
         if (rbits == 0) {
             n_global = hctl.n_over;
         } else {
@@ -328,10 +328,10 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
             WS(o2start, int64_t, "over2.start", B2);
             WS(o2cnt, uint32_t, "over2.cnt", B2);
             WS(o2d1, uint32_t, "over2.d1", B2);
-            k_make_chunks<<<(no + 255) / 256, 256, 0, s>>>(base2, tot2, B2, F2, cap, 1u, rbits,
-                                                          od1, chunks2, &ctl->n_chunks, o2start,
-                                                          o2cnt, o2d1, &ctl->n_over2,
-                                                          &ctl->over2_records);
+            WS(o2hb, uint32_t, "over2.hb", B2);
+            k_make_chunks<<<(no + 255) / 256, 256, 0, s>>>(
+                base2, tot2, B2, F2, cap, 1u, rbits, od1, ohb, pl.plb - rbits, chunks2,
+                &ctl->n_chunks, o2start, o2cnt, o2d1, o2hb, &ctl->n_over2, &ctl->over2_records);
             LAUNCH_CHECK();
             HIP_TRY(hipMemcpyAsync(&hctl, ctl, sizeof(Control), hipMemcpyDeviceToHost, s));
             HIP_TRY(hipStreamSynchronize(s));
@@ -379,13 +379,13 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     if (timing) {
         unsigned long long h[16];
         HIP_TRY(hipMemcpy(h, bpl.phase_cyc, sizeof(h), hipMemcpyDeviceToHost));
-        static const char *nm[9] = {"-", "-", "A.insert", "B.slots", "C.mpc",
+        static const char *nm[9] = {"A0.cas", "A1.count", "A2.barrier", "B.slots", "C.mpc",
                                     "D.state", "E.mcpp", "F.acc", "G.emit"};
         unsigned long long tot = 0;
-        for (int i = 2; i <= 8; ++i) tot += h[i];
+        for (int i = 0; i <= 8; ++i) tot += h[i];
         std::fprintf(stderr, "[dpg phase] chunks=%u over=%u over2=%u per-WG Mcycles:",
                      hctl.n_chunks, hctl.n_over, hctl.n_over2);
-        for (int i = 2; i <= 8; ++i)
+        for (int i = 0; i <= 8; ++i)
             std::fprintf(stderr, " %s=%.3f(%.0f%%)", nm[i], h[i] / 1e6 / G,
                          100.0 * h[i] / (tot ? tot : 1));
         std::fprintf(stderr, "\n");
@@ -474,7 +474,7 @@ int pipeline(dpg_ctx *ctx, hipStream_t s, const int64_t *pid, const int64_t *pk,
                     low_mask(pl.kbits - pl.b1 + pl.pkbits), pl.kbits - pl.b1, &ctl->err};
     int64_t *bstart = nullptr;
     uint32_t *bcnt = nullptr;
-    int r = run_level<SrcSoAKey<R>, R, Ipt<R>::L1, 1024>(ctx, s, s1, 1u, nullptr, nullptr,
+    int r = run_level<SrcSoAKey<R>, R, Ipt<R>::L1, 2048>(ctx, s, s1, 1u, nullptr, nullptr,
                                                          &ctl->n_scalar, n, F1, pl.b1, recA,
                                                          "partition1", &bstart, &bcnt, &ctl->ntiles[0]);
     if (r) return r;
@@ -625,11 +625,17 @@ int dpg_bound_aggregate(dpg_ctx *ctx, const int64_t *pid, const int64_t *pk, con
     pl.kbits = std::max<uint32_t>(1, bits_for(U));
     pl.pkbits = std::max<uint32_t>(1, bits_for((uint64_t)P));
     const uint32_t target = ctx->bucket_target ? ctx->bucket_target : kBucketTarget;
+    // at most 10 pid hash bits may stay below a fine bucket (direct pid slots
+    // in the bound kernel), hence the lower bound kbits - 10
     uint32_t bits_total = bits_for((uint64_t)((n + target - 1) / target));
+    bits_total = std::max<uint32_t>(bits_total, pl.kbits > 10 ? pl.kbits - 10 : 0);
     bits_total = std::max<uint32_t>(1, std::min<uint32_t>(bits_total, kMaxB1 + kMaxB2));
     bits_total = std::min<uint32_t>(bits_total, pl.kbits);
-    pl.b1 = std::min<uint32_t>(kMaxB1, bits_total);
+    // one level up to 11 bits; beyond, the smaller half first (level 1 reads
+    // 16 B per record, so its runs should be the longer ones)
+    pl.b1 = bits_total <= kMaxB1 ? bits_total : bits_total / 2;
     pl.b2 = bits_total - pl.b1;
+    pl.plb = pl.kbits - bits_total;
     const uint32_t ib = std::max<uint32_t>(1, bits_for((uint64_t)n));
     const bool r8 = (pl.kbits - pl.b1) + pl.pkbits + ib <= 64;
     if (r8) return pipeline<R8>(ctx, s, pid, pk, value, n, p, out, ctl, pl, pid_min, U, ib);

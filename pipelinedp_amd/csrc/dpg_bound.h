@@ -153,13 +153,16 @@ __device__ __forceinline__ void cascade_insert(uint64_t *slots, uint32_t k, uint
 }
 
 // Per-pid candidate threshold of the mpc selection: a pid with m > k pairs
-// cascades only the pairs whose 32-bit priority is below ~(2k + 16) / m of
-// the range; the k smallest are among them unless fewer than k fall below,
-// which the completion pass detects (candidate count < k) and completes.
+// cascades only the pairs whose 32-bit priority is below ~e / m of the range,
+// e = k + 3 sqrt(k) + 3 (about 3 sigma above the k-th order statistic); the
+// k smallest keys are among them whenever at least k fall below (any key
+// above the threshold exceeds every candidate's), and the completion pass
+// handles the rest (candidate count < k).  The threshold only steers work:
+// the kept set does not depend on it.
 __device__ __forceinline__ uint32_t cand_threshold(uint32_t m, uint32_t k) {
-    const uint32_t e = 2 * k + 16;
-    if (e >= m) return 0xFFFFFFFFu;
-    return (uint32_t)(((uint64_t)e << 32) / m);
+    const float e = (float)k + 3.0f * sqrtf((float)k) + 3.0f;
+    if (e >= (float)m) return 0xFFFFFFFFu;
+    return (uint32_t)(e / (float)m * 4294967040.0f);
 }
 
 // Wave-aggregated counter allocation; call with the whole wave converged.
@@ -172,7 +175,7 @@ __device__ __forceinline__ uint32_t wave_alloc(T *ctr, bool want, uint32_t per =
     if (b) {
         const int leader = __ffsll((long long)b) - 1;
         if (lane == leader) base = atomicAdd(ctr, (uint32_t)__popcll(b) * per);
-        base = __shfl(base, leader, 64);
+        base = __builtin_amdgcn_readlane(base, leader);
     }
     return base + (uint32_t)__popcll(b & ((1ull << lane) - 1ull)) * per;
 }

@@ -28,26 +28,29 @@ constexpr int kBCap = 1024;          // records per chunk
 constexpr int kRPT = kBCap / kBT;    // records per thread
 constexpr uint32_t kCq = 1024;       // pid table slots (pids <= records)
 constexpr uint32_t kCp = 1024;       // pair table slots (pairs <= records)
-constexpr uint32_t kPool = 2048;     // cascade slots: mpc in [0, 1024), mcpp above
+constexpr uint32_t kPool = 2048;     // selection keys: per-pid regions in [0, 1024), per-pair above
 constexpr uint32_t kMcppBase = 1024;
 constexpr int kQPT = kCq / kBT;      // pid slots per thread
 constexpr int kPPT = kCp / kBT;      // pair slots per thread
 
 struct ChunkShared {
-    uint32_t bump, bump2, nitems, pad;
+    uint32_t bump, bump2, nitems, npair, npid, pad[3];
 };
 
-// LDS layout of one workgroup (KeyT: pair key width).
+// LDS layout of one workgroup (KeyT: pair key width).  Pid slots are direct:
+// q = hash residual - chunk base (< kCq, the chunk packer guarantees it).
 template <class KeyT, class Item>
 struct ChunkLayout {
     static constexpr bool var = ItemTraits<Item>::var;
-    static constexpr size_t PIDTAB = 0;
-    static constexpr size_t PIDM = PIDTAB + 4 * kCq;  // low 16: pairs/records, high: candidates
-    static constexpr size_t PIDSLOT = PIDM + 4 * kCq;
-    static constexpr size_t PAIRTAB = PIDSLOT + 4 * kCq;
+    static constexpr size_t PIDV = 0;                 // privacy id - pid_min
+    static constexpr size_t PIDM = PIDV + 4 * kCq;    // low 16: pairs/records, high: appends
+    static constexpr size_t PIDSLOT = PIDM + 4 * kCq; // pool base (+ appends << 16) or kNil
+    static constexpr size_t QLIST = PIDSLOT + 4 * kCq;  // dense list of occupied pid slots
+    static constexpr size_t PAIRTAB = QLIST + 2 * kCq;
     static constexpr size_t PAIRCNT = PAIRTAB + sizeof(KeyT) * kCp;
     static constexpr size_t PAIRST = PAIRCNT + 4 * kCp;
-    static constexpr size_t POOL = PAIRST + 4 * kCp;
+    static constexpr size_t PLIST = PAIRST + 4 * kCp;  // dense list of occupied pair slots
+    static constexpr size_t POOL = PLIST + 2 * kCp;
     static constexpr size_t ACC = POOL + 8 * kPool;
     static constexpr size_t SH = ACC + 8 * kCp * (var ? 3 : 1);
     static constexpr size_t TOTAL = SH + sizeof(ChunkShared);
@@ -55,18 +58,15 @@ struct ChunkLayout {
     static_assert(TOTAL <= 80 * 1024, "chunk working set too large");
 };
 
+// Full clear (kernel start); chunks clear only their occupied slots.
 template <class KeyT, class Item>
 __device__ __forceinline__ void clear_tables(char *smem) {
     using L = ChunkLayout<KeyT, Item>;
-    uint32_t *pidtab = reinterpret_cast<uint32_t *>(smem + L::PIDTAB);
     uint32_t *pidm = reinterpret_cast<uint32_t *>(smem + L::PIDM);
     KeyT *pairtab = reinterpret_cast<KeyT *>(smem + L::PAIRTAB);
     uint32_t *paircnt = reinterpret_cast<uint32_t *>(smem + L::PAIRCNT);
 #pragma unroll
-    for (int j = 0; j < kQPT; ++j) {
-        pidtab[threadIdx.x + j * kBT] = kEmpty32;
-        pidm[threadIdx.x + j * kBT] = 0;
-    }
+    for (int j = 0; j < kQPT; ++j) pidm[threadIdx.x + j * kBT] = 0;
 #pragma unroll
     for (int j = 0; j < kPPT; ++j) {
         pairtab[threadIdx.x + j * kBT] = empty_key<KeyT>();
@@ -74,19 +74,116 @@ __device__ __forceinline__ void clear_tables(char *smem) {
     }
 }
 
+// Linear probing continued from slot h (the home slot's CAS already failed on
+// a different key); `won` = this lane created the entry.
+template <class K>
+__device__ __forceinline__ uint32_t probe_from(K *keys, uint32_t mask, K key, uint32_t h,
+                                               bool &won, uint32_t *err) {
+    for (uint32_t probe = 1; probe <= mask; ++probe) {
+        h = (h + 1) & mask;
+        K old;
+        if constexpr (sizeof(K) == 8)
+            old = (K)atomicCAS((unsigned long long *)&keys[h], (unsigned long long)empty_key<K>(),
+                               (unsigned long long)key);
+        else
+            old = atomicCAS(&keys[h], empty_key<K>(), key);
+        if (old == empty_key<K>()) {
+            won = true;
+            return h;
+        }
+        if (old == key) {
+            won = false;
+            return h;
+        }
+    }
+    atomicOr(err, 2u);
+    won = false;
+    return 0;
+}
+
+template <class K>
+__device__ __forceinline__ K cas_home(K *keys, uint32_t h, K key) {
+    if constexpr (sizeof(K) == 8)
+        return (K)atomicCAS((unsigned long long *)&keys[h], (unsigned long long)empty_key<K>(),
+                            (unsigned long long)key);
+    else
+        return atomicCAS(&keys[h], empty_key<K>(), key);
+}
+
+// Variable-size wave-aggregated allocation (amount 0: nothing); call with
+// the whole wave converged.
+template <class T>
+__device__ __forceinline__ uint32_t wave_alloc_var(T *ctr, uint32_t amount) {
+    uint32_t total;
+    const uint32_t ex = wave_excl_scan(amount, total);
+    uint32_t base = 0;
+    if (total) {
+        if (__lane_id() == 0) base = atomicAdd(ctr, total);
+        base = __shfl(base, 0, 64);
+    }
+    return base + ex;
+}
+
+// Batched wave-aggregated allocation: lane slot k gets one entry where
+// want[k]; one LDS atomic per wave for all K (call with the wave converged).
+__device__ __forceinline__ uint32_t lanes_below(uint64_t b) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
+                                     __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+}
+template <int K>
+__device__ __forceinline__ void wave_alloc_batch(uint32_t *ctr, const bool (&want)[K],
+                                                 uint32_t (&slot)[K]) {
+    uint64_t b[K];
+    uint32_t tot = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        b[k] = __ballot(want[k]);
+        tot += (uint32_t)__popcll(b[k]);
+    }
+    uint32_t base = 0;
+    if (tot) {
+        if (__lane_id() == 0) base = atomicAdd(ctr, tot);
+        base = __builtin_amdgcn_readfirstlane(base);
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        slot[k] = base + lanes_below(b[k]);
+        base += (uint32_t)__popcll(b[k]);
+    }
+}
+
+// Number of keys in a[0, cnt) below x (cnt >= 1): loads are unconditional
+// (index clamped) in batches of 8 so that a batch is in flight together.
+__device__ __forceinline__ uint32_t rank_below(const uint64_t *a, uint32_t cnt, uint64_t x) {
+    uint32_t r = 0;
+    for (uint32_t j = 0; j < cnt; j += 8) {
+        uint64_t y[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) y[u] = a[min(j + u, cnt - 1)];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) r += (j + u < cnt && y[u] < x) ? 1u : 0u;
+    }
+    return r;
+}
+
+// Records past the chunk end hold a copy of its last record (loads are
+// unconditional): they take part in the table inserts, whose keys exist
+// anyway, and in nothing that counts.
 template <class KeyT, class Item, class R>
 __device__ __forceinline__ void bound_chunk(const R (&r)[kRPT], uint32_t n, uint32_t d1,
-                                            const R *next_base, uint32_t next_n,
+                                            uint32_t hbase, const R *next_base, uint32_t next_n,
                                             R (&rn)[kRPT], char *smem, const BoundParams &bp,
                                             Item *items, PhaseTimer &clk) {
     using L = ChunkLayout<KeyT, Item>;
     constexpr bool kVar = L::var;
-    uint32_t *pidtab = reinterpret_cast<uint32_t *>(smem + L::PIDTAB);
+    uint32_t *pidv = reinterpret_cast<uint32_t *>(smem + L::PIDV);
     uint32_t *pidm = reinterpret_cast<uint32_t *>(smem + L::PIDM);
     uint32_t *pidslot = reinterpret_cast<uint32_t *>(smem + L::PIDSLOT);
+    uint16_t *qlist = reinterpret_cast<uint16_t *>(smem + L::QLIST);
     KeyT *pairtab = reinterpret_cast<KeyT *>(smem + L::PAIRTAB);
     uint32_t *paircnt = reinterpret_cast<uint32_t *>(smem + L::PAIRCNT);
     uint32_t *pairst = reinterpret_cast<uint32_t *>(smem + L::PAIRST);
+    uint16_t *plist = reinterpret_cast<uint16_t *>(smem + L::PLIST);
     uint64_t *pool = reinterpret_cast<uint64_t *>(smem + L::POOL);
     double *acc_sum = reinterpret_cast<double *>(smem + L::ACC);
     double *acc_nsum = acc_sum + kCp;
@@ -103,47 +200,88 @@ __device__ __forceinline__ void bound_chunk(const R (&r)[kRPT], uint32_t n, uint
     const bool part_clip = bp.sum_mode == DPG_SUM_CLIP_PARTITION;
     const uint32_t lim = per_pid ? bp.L : bp.mpc;
 
-    // ---- A: pid and pair inserts, counts (record-major)
+    // ---- A: pair inserts and counts (record-major); the pid slot is the
+    // hash residual minus the chunk base.  The home-slot CAS of all kRPT
+    // records is issued back to back; only collisions probe on.  Lanes past
+    // the chunk end aim their CAS at a lane-private dummy word in the (still
+    // idle) pool, so they neither touch the table nor serialise on one
+    // address.  The first pair (record, PER_PRIVACY_ID) of a pid appends the
+    // pid slot to the dense pid list.
     uint32_t qs[kRPT], ps[kRPT];
+    bool valid[kRPT];
+    {
+        KeyT pkey[kRPT], op[kRPT];
 #pragma unroll
-    for (int k = 0; k < kRPT; ++k) {
-        const uint32_t i = tid + k * kBT;
-        qs[k] = ps[k] = 0;
-        if (i < n) {
+        for (int k = 0; k < kRPT; ++k) {
+            valid[k] = tid + k * kBT < n;
             const uint64_t key = RecOps<R>::key(r[k], f);
-            bool wq, wp;
-            qs[k] = insert_key<uint32_t>(pidtab, kCq - 1, (uint32_t)(key >> pkb), wq, bp.err);
-            if (per_pid) atomicAdd(&pidm[qs[k]], 1u);
-            const KeyT pkey = ((KeyT)qs[k] << pkb) | (KeyT)(key & pkmask);
-            ps[k] = insert_key<KeyT>(pairtab, kCp - 1, pkey, wp, bp.err);
-            atomicAdd(&paircnt[ps[k]], 1u);
-            if (!per_pid && wp) atomicAdd(&pidm[qs[k]], 1u);
+            qs[k] = ((uint32_t)(key >> pkb) - hbase) & (kCq - 1);
+            pkey[k] = ((KeyT)qs[k] << pkb) | (KeyT)(key & pkmask);
+            ps[k] = hslot(pkey[k], kCp - 1);
+            KeyT *tgt = valid[k] ? pairtab + ps[k]
+                                 : reinterpret_cast<KeyT *>(pool) + (tid + k * kBT);
+            op[k] = cas_home<KeyT>(tgt, 0, pkey[k]);
         }
+        mark(bp, 0, clk);
+        bool won[kRPT], first[kRPT];
+        uint32_t oldm[kRPT];
+#pragma unroll
+        for (int k = 0; k < kRPT; ++k) {
+            won[k] = valid[k] && op[k] == empty_key<KeyT>();
+            if (valid[k] && !won[k] && op[k] != pkey[k])
+                ps[k] = probe_from<KeyT>(pairtab, kCp - 1, pkey[k], ps[k], won[k], bp.err);
+        }
+        // counts; the returned pid count (all kRPT in flight together; lanes
+        // not counting add 0 to a valid slot) tells the pid's first toucher
+#pragma unroll
+        for (int k = 0; k < kRPT; ++k) {
+            if (valid[k]) atomicAdd(&paircnt[ps[k]], 1u);
+            const bool touch = per_pid ? valid[k] : won[k];
+            oldm[k] = atomicAdd(&pidm[qs[k]], touch ? 1u : 0u);
+        }
+#pragma unroll
+        for (int k = 0; k < kRPT; ++k) first[k] = (per_pid ? valid[k] : won[k]) && oldm[k] == 0u;
+        uint32_t qi[kRPT], li[kRPT];
+        wave_alloc_batch<kRPT>(&sh->npid, first, qi);
+        wave_alloc_batch<kRPT>(&sh->npair, won, li);
+#pragma unroll
+        for (int k = 0; k < kRPT; ++k) {
+            if (first[k]) qlist[qi[k]] = (uint16_t)qs[k];
+            if (won[k]) plist[li[k]] = (uint16_t)ps[k];
+        }
+        mark(bp, 1, clk);
     }
     __syncthreads();
     mark(bp, 2, clk);
     // prefetch the next chunk's records (in flight during the phases below)
+    if (next_n > 0) {
 #pragma unroll
-    for (int k = 0; k < kRPT; ++k) {
-        const uint32_t i = tid + k * kBT;
-        if (i < next_n) rn[k] = next_base[i];
+        for (int k = 0; k < kRPT; ++k) rn[k] = next_base[min((uint32_t)(tid + k * kBT), next_n - 1)];
     }
-    // ---- B: cascade slots for pids over their limit (pid-major); pair
-    // accumulators / counters (pair-major)
+    const uint32_t npair = __builtin_amdgcn_readfirstlane(sh->npair);
+    const uint32_t npid = __builtin_amdgcn_readfirstlane(sh->npid);
+    // ---- B: privacy id of every pid (pid-major, dense) and, for pids over
+    // their limit, one pool slot per pair (per record in PER_PRIVACY_ID
+    // mode) for the selection keys; pair accumulators (pair-major, dense)
+    const uint32_t hshift = f.kbits - f.b1;
 #pragma unroll
     for (int j = 0; j < kQPT; ++j) {
-        const uint32_t q = tid + j * kBT;
-        const bool occ = pidtab[q] != kEmpty32;
-        const bool want = occ && (pidm[q] & 0xFFFFu) > lim;
-        const uint32_t s = wave_alloc(&sh->bump, want, lim);
-        if (want)
-            for (uint32_t t = 0; t < lim; ++t) pool[s + t] = kEmpty64;
-        if (occ) pidslot[q] = want ? s : kNil;
+        const uint32_t li = tid + j * kBT;
+        const bool occ = li < npid;
+        const uint32_t q = occ ? qlist[li] : 0u;
+        const uint32_t m = occ ? (pidm[q] & 0xFFFFu) : 0u;
+        const bool want = m > lim;
+        const uint32_t s = want ? atomicAdd(&sh->bump, m) : 0u;
+        if (occ) {
+            pidslot[q] = want ? s : kNil;
+            pidv[q] = hk_inv((d1 << hshift) | (hbase + q), bp.hash);
+        }
     }
 #pragma unroll
     for (int j = 0; j < kPPT; ++j) {
-        const uint32_t p = tid + j * kBT;
-        if (pairtab[p] == empty_key<KeyT>()) continue;
+        const uint32_t li = tid + j * kBT;
+        if (li >= npair) continue;
+        const uint32_t p = plist[li];
         if (need_v) {
             acc_sum[p] = 0.0;
             if (kVar) {
@@ -157,74 +295,96 @@ __device__ __forceinline__ void bound_chunk(const R (&r)[kRPT], uint32_t n, uint
     mark(bp, 3, clk);
 
     bool emit[kPPT];
-    uint32_t ecnt[kPPT];
+    uint32_t ecnt[kPPT], pslot_of[kPPT];
     if (!per_pid) {
-        // ---- C: mpc cascade over pair keys (pair-major): candidates first,
-        // then the rare completion pass for pids with < mpc candidates
+        // ---- C1: mpc selection over pair keys (pair-major, dense): pairs of
+        // over-limit pids whose priority is below the candidate threshold
+        // append their key to the pid's pool region
         uint64_t k64[kPPT];
-        uint32_t pslot[kPPT];
-        bool over[kPPT], cand[kPPT];
+        uint32_t pbase[kPPT];
+        bool over[kPPT], cand[kPPT], kept[kPPT];
 #pragma unroll
         for (int j = 0; j < kPPT; ++j) {
-            const uint32_t p = tid + j * kBT;
-            const KeyT pkey = pairtab[p];
+            const uint32_t li = tid + j * kBT;
             over[j] = cand[j] = false;
+            kept[j] = li < npair;
             k64[j] = 0;
-            pslot[j] = kNil;
-            if (pkey == empty_key<KeyT>()) continue;
+            pbase[j] = 0;
+            pslot_of[j] = 0;
+            if (li >= npair) continue;
+            const uint32_t p = plist[li];
+            pslot_of[j] = p;
+            const KeyT pkey = pairtab[p];
             const uint32_t q = (uint32_t)(pkey >> pkb);
             const uint32_t s = pidslot[q];
-            pslot[j] = s;
             if (s == kNil) continue;
             over[j] = true;
+            pbase[j] = s;
             const uint32_t pk = (uint32_t)(pkey & (KeyT)pkmask);
-            const uint32_t pr = pair_prio(bp.seed, pid_of(bp, d1, pidtab[q]), pk);
+            const uint32_t pr =
+                pair_prio(bp.seed, (uint64_t)(bp.pid_min + (int64_t)pidv[q]), pk);
             k64[j] = ((uint64_t)pr << 32) | pk;
             cand[j] = pr < cand_threshold(pidm[q] & 0xFFFFu, bp.mpc);
-            if (cand[j]) {
-                cascade_insert(pool + s, bp.mpc, k64[j]);
-                atomicAdd(&pidm[q], 1u << 16);
+            if (cand[j]) pool[s + (atomicAdd(&pidm[q], 1u << 16) >> 16)] = k64[j];
+        }
+        __syncthreads();
+        // ---- C2: with >= mpc candidates a candidate is kept iff fewer than
+        // mpc candidates have a smaller key (every non-candidate key exceeds
+        // every candidate key); with fewer (rare), all candidates are kept and
+        // the non-candidates append after them for C3
+        uint32_t ncd[kPPT];
+#pragma unroll
+        for (int j = 0; j < kPPT; ++j) {
+            ncd[j] = 0;
+            if (!over[j]) continue;
+            const uint32_t q = (uint32_t)(pairtab[pslot_of[j]] >> pkb);
+            const uint32_t nc = pidm[q] >> 16;
+            ncd[j] = nc;
+            if (nc >= bp.mpc) {
+                kept[j] = cand[j] && rank_below(pool + pbase[j], nc, k64[j]) < bp.mpc;
+            } else if (!cand[j]) {
+                pool[pbase[j] + nc + (atomicAdd(&pidslot[q], 1u << 16) >> 16)] = k64[j];
             }
         }
         __syncthreads();
-#pragma unroll
-        for (int j = 0; j < kPPT; ++j) {
-            if (!over[j] || cand[j]) continue;
-            const uint32_t q = (uint32_t)(pairtab[tid + j * kBT] >> pkb);
-            if ((pidm[q] >> 16) < bp.mpc) cascade_insert(pool + pslot[j], bp.mpc, k64[j]);
-        }
-        __syncthreads();
         mark(bp, 4, clk);
-        // ---- D: pair state; mcpp cascade slots for over-full kept pairs
+        // ---- D: (C3) non-candidates of pids short of candidates rank among
+        // the appended non-candidates; pair state; every over-full kept pair
+        // reserves one pool slot per record for its record keys
 #pragma unroll
         for (int j = 0; j < kPPT; ++j) {
-            const uint32_t p = tid + j * kBT;
-            const bool occ = pairtab[p] != empty_key<KeyT>();
-            const bool kept = occ && (!over[j] || k64[j] <= pool[pslot[j] + bp.mpc - 1]);
+            const uint32_t li = tid + j * kBT;
+            const bool occ = li < npair;
+            const uint32_t p = pslot_of[j];
+            if (over[j] && !cand[j] && ncd[j] < bp.mpc) {
+                const uint32_t q = (uint32_t)(pairtab[p] >> pkb);
+                const uint32_t nn = pidslot[q] >> 16;
+                kept[j] = rank_below(pool + pbase[j] + ncd[j], nn, k64[j]) < bp.mpc - ncd[j];
+            }
             const uint32_t c = occ ? paircnt[p] : 0u;
-            const bool need = sample && kept && c > bp.mcpp;
-            const uint32_t b2 = wave_alloc(&sh->bump2, need, bp.mcpp);
-            if (need)
-                for (uint32_t t = 0; t < bp.mcpp; ++t) pool[b2 + t] = kEmpty64;
-            if (occ) pairst[p] = !kept ? kDropped : (need ? b2 : kKeptAll);
-            emit[j] = kept;
+            const bool need = sample && kept[j] && c > bp.mcpp;
+            const uint32_t b2 = need ? atomicAdd(&sh->bump2, c) : 0u;
+            if (occ) pairst[p] = !kept[j] ? kDropped : (need ? b2 : kKeptAll);
+            emit[j] = kept[j];
             ecnt[j] = bp.mode == DPG_MODE_CROSS_AND_PER_PARTITION ? min(c, bp.mcpp) : c;
         }
         __syncthreads();
         mark(bp, 5, clk);
-        // ---- E: mcpp cascade over record keys inside over-full kept pairs;
-        // the values of records of kept pairs are gathered meanwhile
+        // ---- E: records of over-full kept pairs append their record key to
+        // the pair's pool region (the low 16 bits of pairst hold its base, the
+        // high 16 count appends); the values of records of kept pairs are
+        // gathered meanwhile
         uint64_t rkey[kRPT];
         double v[kRPT];
         uint32_t st[kRPT];
 #pragma unroll
         for (int k = 0; k < kRPT; ++k) {
-            const uint32_t i = tid + k * kBT;
             rkey[k] = 0;
             v[k] = 0.0;
-            st[k] = kDropped;
-            if (i >= n) continue;
-            st[k] = pairst[ps[k]];
+            // other records of the pair may already have appended (high 16
+            // bits), so a sampled pair's base is the low 16 bits
+            st[k] = valid[k] ? pairst[ps[k]] : kDropped;
+            if (st[k] < kKeptAll) st[k] &= 0xFFFFu;
             if (need_v && st[k] != kDropped) v[k] = bp.value[RecOps<R>::idx(r[k], f)];
         }
         if (sample) {
@@ -232,20 +392,23 @@ __device__ __forceinline__ void bound_chunk(const R (&r)[kRPT], uint32_t n, uint
             for (int k = 0; k < kRPT; ++k) {
                 if (st[k] >= kKeptAll) continue;
                 const uint64_t key = RecOps<R>::key(r[k], f);
-                rkey[k] = rec_prio(bp.seed, pid_of(bp, d1, pidtab[qs[k]]),
+                rkey[k] = rec_prio(bp.seed, (uint64_t)(bp.pid_min + (int64_t)pidv[qs[k]]),
                                    (uint32_t)(key & pkmask),
                                    (uint64_t)(bp.rec_base + RecOps<R>::idx(r[k], f)));
-                cascade_insert(pool + st[k], bp.mcpp, rkey[k]);
+                pool[st[k] + (atomicAdd(&pairst[ps[k]], 1u << 16) >> 16)] = rkey[k];
             }
             __syncthreads();
         }
         mark(bp, 6, clk);
-        // ---- F: accumulators of kept records
+        // ---- F: a sampled record is kept iff fewer than mcpp records of its
+        // pair have a smaller key; accumulators of kept records
         if (need_v) {
 #pragma unroll
             for (int k = 0; k < kRPT; ++k) {
                 if (st[k] == kDropped) continue;
-                if (st[k] != kKeptAll && rkey[k] > pool[st[k] + bp.mcpp - 1]) continue;
+                if (st[k] != kKeptAll &&
+                    rank_below(pool + st[k], paircnt[ps[k]], rkey[k]) >= bp.mcpp)
+                    continue;
                 const uint32_t p = ps[k];
                 if (part_clip) {
                     atomicAdd(&acc_sum[p], v[k]);
@@ -263,30 +426,31 @@ __device__ __forceinline__ void bound_chunk(const R (&r)[kRPT], uint32_t n, uint
         }
         mark(bp, 7, clk);
     } else {
-        // ---- PER_PRIVACY_ID: keep the L records of each pid with the
-        // smallest record key; pairst counts kept records per pair
+        // ---- PER_PRIVACY_ID: records of pids over L append their record key
+        // to the pid's pool region; a record is kept iff fewer than L records
+        // of its pid have a smaller key; pairst counts kept records per pair
         uint64_t rkey[kRPT];
         uint32_t s[kRPT];
 #pragma unroll
         for (int k = 0; k < kRPT; ++k) {
-            const uint32_t i = tid + k * kBT;
             rkey[k] = 0;
             s[k] = kNil;
-            if (i >= n) continue;
+            if (!valid[k]) continue;
             s[k] = pidslot[qs[k]];
             if (s[k] == kNil) continue;
             const uint64_t key = RecOps<R>::key(r[k], f);
-            rkey[k] = rec_prio(bp.seed, pid_of(bp, d1, pidtab[qs[k]]), (uint32_t)(key & pkmask),
+            rkey[k] = rec_prio(bp.seed, (uint64_t)(bp.pid_min + (int64_t)pidv[qs[k]]),
+                               (uint32_t)(key & pkmask),
                                (uint64_t)(bp.rec_base + RecOps<R>::idx(r[k], f)));
-            cascade_insert(pool + s[k], bp.L, rkey[k]);
+            pool[s[k] + (atomicAdd(&pidm[qs[k]], 1u << 16) >> 16)] = rkey[k];
         }
         __syncthreads();
         mark(bp, 5, clk);
 #pragma unroll
         for (int k = 0; k < kRPT; ++k) {
-            const uint32_t i = tid + k * kBT;
-            if (i >= n) continue;
-            if (s[k] != kNil && rkey[k] > pool[s[k] + bp.L - 1]) continue;
+            if (!valid[k]) continue;
+            if (s[k] != kNil && rank_below(pool + s[k], pidm[qs[k]] & 0xFFFFu, rkey[k]) >= bp.L)
+                continue;
             const uint32_t p = ps[k];
             atomicAdd(&pairst[p], 1u);
             if (need_v) {
@@ -308,17 +472,20 @@ __device__ __forceinline__ void bound_chunk(const R (&r)[kRPT], uint32_t n, uint
         mark(bp, 7, clk);
 #pragma unroll
         for (int j = 0; j < kPPT; ++j) {
-            const uint32_t p = tid + j * kBT;
-            const bool occ = pairtab[p] != empty_key<KeyT>();
-            ecnt[j] = occ ? pairst[p] : 0u;
+            const uint32_t li = tid + j * kBT;
+            pslot_of[j] = li < npair ? plist[li] : 0u;
+            ecnt[j] = li < npair ? pairst[pslot_of[j]] : 0u;
             emit[j] = ecnt[j] > 0;
         }
     }
-    // ---- G: emit kept pairs (pair-major); clear the tables for the next chunk
+    // ---- G: emit kept pairs (pair-major, dense); clear the tables for the
+    // next chunk
+    uint32_t islot[kPPT];
+    wave_alloc_batch<kPPT>(&sh->nitems, emit, islot);
 #pragma unroll
     for (int j = 0; j < kPPT; ++j) {
-        const uint32_t p = tid + j * kBT;
-        const uint32_t slot = wave_alloc(&sh->nitems, emit[j]);
+        const uint32_t p = pslot_of[j];
+        const uint32_t slot = islot[j];
         if (!emit[j]) continue;
         Item it;
         it.pk = (uint32_t)(pairtab[p] & (KeyT)pkmask);
@@ -336,17 +503,29 @@ __device__ __forceinline__ void bound_chunk(const R (&r)[kRPT], uint32_t n, uint
         items[slot] = it;
     }
     __syncthreads();
-    clear_tables<KeyT, Item>(smem);
+    // clear the occupied slots for the next chunk
+#pragma unroll
+    for (int j = 0; j < kPPT; ++j) {
+        const uint32_t li = tid + j * kBT;
+        if (li < npair) {
+            const uint32_t p = plist[li];
+            pairtab[p] = empty_key<KeyT>();
+            paircnt[p] = 0;
+        }
+        if (li < npid) pidm[qlist[li]] = 0;
+    }
     if (tid == 0) {
         sh->bump = 0;
         sh->bump2 = kMcppBase;
+        sh->npair = 0;
+        sh->npid = 0;
     }
     __syncthreads();
     mark(bp, 8, clk);
 }
 
 // Chunk descriptor: records [x, x + (y & 0x7FFFFFFF)) of buffer (y >> 31),
-// level-1 bucket z.
+// level-1 bucket z, pid hash-residual base w.
 template <class R>
 __device__ __forceinline__ const R *chunk_base(uint4 d, const R *b0, const R *b1) {
     return ((d.y >> 31) ? b1 : b0) + d.x;
@@ -375,24 +554,24 @@ __global__ __launch_bounds__(kBT) void k_bound_chunks(const R *recs, const R *re
         sh->bump = 0;
         sh->bump2 = kMcppBase;
         sh->nitems = 0;
+        sh->npair = 0;
+        sh->npid = 0;
     }
     // software pipeline: records of chunk w in r, descriptor of w + G in dn;
     // the descriptor of w + 2G and the records of w + G load during w
     R r[kRPT], rn[kRPT];
     const uint32_t G = gridDim.x;
     uint32_t w = blockIdx.x;
-    uint32_t n = 0, d1 = 0;
+    uint32_t n = 0, d1 = 0, hb = 0;
     uint4 dn = make_uint4(0, 0, 0, 0);
     if (w < nch) {
         const uint4 d = chunks[w];
         n = __builtin_amdgcn_readfirstlane(d.y & 0x7FFFFFFFu);
         d1 = __builtin_amdgcn_readfirstlane(d.z);
+        hb = __builtin_amdgcn_readfirstlane(d.w);
         const R *b = chunk_base(d, recs, refined);
 #pragma unroll
-        for (int k = 0; k < kRPT; ++k) {
-            const uint32_t i = threadIdx.x + k * kBT;
-            if (i < n) r[k] = b[i];
-        }
+        for (int k = 0; k < kRPT; ++k) r[k] = b[min((uint32_t)(threadIdx.x + k * kBT), n - 1)];
         if (w + G < nch) dn = chunks[w + G];
     }
     __syncthreads();
@@ -401,14 +580,16 @@ __global__ __launch_bounds__(kBT) void k_bound_chunks(const R *recs, const R *re
         if (w + 2 * G < nch) dnn = chunks[w + 2 * G];
         const uint4 du = make_uint4(__builtin_amdgcn_readfirstlane(dn.x),
                                     __builtin_amdgcn_readfirstlane(dn.y),
-                                    __builtin_amdgcn_readfirstlane(dn.z), 0u);
+                                    __builtin_amdgcn_readfirstlane(dn.z),
+                                    __builtin_amdgcn_readfirstlane(dn.w));
         const uint32_t nn = du.y & 0x7FFFFFFFu;
-        bound_chunk<KeyT, Item, R>(r, n, d1, chunk_base(du, recs, refined), nn, rn, smem, bp,
-                                   my_items, clk);
+        bound_chunk<KeyT, Item, R>(r, n, d1, hb, chunk_base(du, recs, refined), nn, rn, smem,
+                                   bp, my_items, clk);
 #pragma unroll
         for (int k = 0; k < kRPT; ++k) r[k] = rn[k];
         n = nn;
         d1 = du.z;
+        hb = du.w;
         dn = dnn;
     }
     if (threadIdx.x == 0) wg_cnt[blockIdx.x] = sh->nitems;
@@ -447,30 +628,39 @@ __global__ __launch_bounds__(1024) void k_scan_small(const uint32_t *in, uint32_
 
 // Greedy packing of consecutive fine buckets into chunks of <= cap records,
 // one thread per group of `group` buckets; a group never spans two level-1
-// buckets: bucket b belongs to level-1 bucket b >> d1_shift, or to
-// d1_map[b >> d1_shift] when a map is given (refined buckets), and group
-// divides 1 << d1_shift.  Buckets larger than cap go to the oversize list
-// (start, count, level-1 bucket).  sel = buffer the buckets live in.
+// buckets: bucket b belongs to level-1 bucket b >> d1_shift (group divides
+// 1 << d1_shift), or to d1_map[b >> d1_shift] for refined buckets.  A
+// bucket's pid hash-residual base is (b mod 2^d1_shift) << plb (plus
+// hb_map[b >> d1_shift] for refined buckets); a chunk spans at most
+// kCq >> plb bucket indices, so its pid slots (residual - chunk base) stay
+// below kCq.  Buckets larger than cap go to the oversize list (start, count,
+// level-1 bucket, residual base).  sel = buffer the buckets live in.
 __global__ void k_make_chunks(const int64_t *bstart, const uint32_t *bcnt, uint32_t B,
                               uint32_t group, uint32_t cap, uint32_t sel, uint32_t d1_shift,
-                              const uint32_t *d1_map, uint4 *chunks, uint32_t *n_chunks,
-                              int64_t *over_start, uint32_t *over_cnt, uint32_t *over_d1,
+                              const uint32_t *d1_map, const uint32_t *hb_map, uint32_t plb,
+                              uint4 *chunks, uint32_t *n_chunks, int64_t *over_start,
+                              uint32_t *over_cnt, uint32_t *over_d1, uint32_t *over_hb,
                               uint32_t *n_over, unsigned long long *over_records) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t b0 = g * group;
     if (b0 >= B) return;
     const uint32_t b1 = min(B, b0 + group);
+    const uint32_t maxspan = kCq >> plb;
+    const uint32_t lmask = (1u << d1_shift) - 1u;
+    const uint32_t d1 = d1_map ? d1_map[b0 >> d1_shift] : (b0 >> d1_shift);
+    const uint32_t hb0 = hb_map ? hb_map[b0 >> d1_shift] : 0u;
     // pass 1: count chunks
-    uint32_t nc = 0, cur = 0;
+    uint32_t nc = 0, cur = 0, bfirst = 0;
     int64_t cend = -1;
     for (uint32_t b = b0; b < b1; ++b) {
         const uint32_t c = bcnt[b];
         if (c == 0) continue;
         if (c > cap) continue;
         const int64_t st = bstart[b];
-        if (cur == 0 || cur + c > cap || st != cend) {
+        if (cur == 0 || cur + c > cap || st != cend || b - bfirst >= maxspan) {
             ++nc;
             cur = 0;
+            bfirst = b;
         }
         cur += c;
         cend = st + c;
@@ -479,29 +669,36 @@ __global__ void k_make_chunks(const int64_t *bstart, const uint32_t *bcnt, uint3
     // pass 2: write
     cur = 0;
     cend = -1;
+    bfirst = 0;
     int64_t cst = 0;
-    const uint32_t d1 = d1_map ? d1_map[b0 >> d1_shift] : (b0 >> d1_shift);
     for (uint32_t b = b0; b < b1; ++b) {
         const uint32_t c = bcnt[b];
         if (c == 0) continue;
         const int64_t st = bstart[b];
+        const uint32_t hb = hb0 + ((b & lmask) << plb);
         if (c > cap) {
             const uint32_t o = atomicAdd(n_over, 1u);
             over_start[o] = st;
             over_cnt[o] = c;
             over_d1[o] = d1;
+            over_hb[o] = hb;
             atomicAdd(over_records, (unsigned long long)c);
             continue;
         }
-        if (cur == 0 || cur + c > cap || st != cend) {
-            if (cur) chunks[base++] = make_uint4((uint32_t)cst, cur | (sel << 31), d1, 0u);
+        if (cur == 0 || cur + c > cap || st != cend || b - bfirst >= maxspan) {
+            if (cur)
+                chunks[base++] = make_uint4((uint32_t)cst, cur | (sel << 31), d1,
+                                            hb0 + ((bfirst & lmask) << plb));
             cur = 0;
             cst = st;
+            bfirst = b;
         }
         cur += c;
         cend = st + c;
     }
-    if (cur) chunks[base++] = make_uint4((uint32_t)cst, cur | (sel << 31), d1, 0u);
+    if (cur)
+        chunks[base++] =
+            make_uint4((uint32_t)cst, cur | (sel << 31), d1, hb0 + ((bfirst & lmask) << plb));
 }
 
 }  // namespace dpg

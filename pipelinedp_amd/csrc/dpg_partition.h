@@ -379,13 +379,30 @@ __global__ __launch_bounds__(kPartThreads) void k_scatter(Src src_in, const Tile
         const uint32_t lim = (uint32_t)min<int64_t>(SUB, td.end - sb);  // uniform
         Rec rec[IPT];
         uint32_t dr[IPT];  // digit | rank << 12, or ~0 for a dropped record
+        if (bits > 4) {
+            // wide fan-out: one LDS atomic per record ranks it (order inside
+            // a digit is free); all IPT atomics are in flight together
 #pragma unroll
-        for (int j = 0; j < IPT; ++j) {
-            const uint32_t o = j * kPartThreads + tid;
-            uint32_t d = 0;
-            const bool ok = o < lim && src.decode(raw[j], sb + o, rec[j], d);
-            const uint32_t rk = wave_agg_rank(cnt, ok ? d : 0u, ok, bits);
-            dr[j] = ok ? (d | (rk << 12)) : ~0u;
+            for (int j = 0; j < IPT; ++j) {
+                const uint32_t o = j * kPartThreads + tid;
+                uint32_t d = 0;
+                const bool ok = o < lim && src.decode(raw[j], sb + o, rec[j], d);
+                dr[j] = ok ? d : ~0u;
+            }
+#pragma unroll
+            for (int j = 0; j < IPT; ++j)
+                if (dr[j] != ~0u) dr[j] |= atomicAdd(&cnt[dr[j]], 1u) << 12;
+        } else {
+            // few digits: wave-aggregated ranking avoids same-address
+            // serialisation
+#pragma unroll
+            for (int j = 0; j < IPT; ++j) {
+                const uint32_t o = j * kPartThreads + tid;
+                uint32_t d = 0;
+                const bool ok = o < lim && src.decode(raw[j], sb + o, rec[j], d);
+                const uint32_t rk = wave_agg_rank(cnt, ok ? d : 0u, ok, bits);
+                dr[j] = ok ? (d | (rk << 12)) : ~0u;
+            }
         }
         __syncthreads();
         const uint32_t total = block_scan_digits(cnt, dstart, F, sh16);
@@ -405,12 +422,25 @@ __global__ __launch_bounds__(kPartThreads) void k_scatter(Src src_in, const Tile
             for (int j = 0; j < IPT; ++j)
                 raw[j] = src.fetch(nb + min((uint32_t)(j * kPartThreads + tid), nlim - 1));
         }
-        for (uint32_t k = tid; k < total; k += kPartThreads) {
-            const W x = stage[k];
-            uint32_t dd;
-            if constexpr (kSD) dd = sdig[k];
-            else dd = src.digit(from_words<Rec>(x));
-            *reinterpret_cast<W *>(&out[(size_t)cur[dd] + (k - dstart[dd])]) = x;
+        // write-out in batches of WB staged records per thread: the LDS reads
+        // of a batch are in flight together, stores are predicated
+        constexpr int WB = IPT < 8 ? IPT : 8;
+        for (uint32_t k0 = 0; k0 < total; k0 += WB * kPartThreads) {
+            W x[WB];
+            uint32_t dd[WB];
+#pragma unroll
+            for (int u = 0; u < WB; ++u) {
+                const uint32_t k = min(k0 + u * kPartThreads + tid, total - 1);
+                x[u] = stage[k];
+                if constexpr (kSD) dd[u] = sdig[k];
+                else dd[u] = src.digit(from_words<Rec>(x[u]));
+            }
+#pragma unroll
+            for (int u = 0; u < WB; ++u) {
+                const uint32_t k = k0 + u * kPartThreads + tid;
+                const uint32_t dst = cur[dd[u]] - dstart[dd[u]] + k;
+                if (k < total) *reinterpret_cast<W *>(&out[dst]) = x[u];
+            }
         }
         __syncthreads();
         for (uint32_t d = tid; d < F; d += kPartThreads) {
