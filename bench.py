@@ -177,7 +177,8 @@ def main():
     algo_bytes = ALGO_BYTES_PER_RECORD * args.records
     # dominant kernel: the longest single-kernel stage (each of these stage
     # names brackets exactly one launch on the stream the kernels run on)
-    kernels = {"bound": "k_bound_chunks", "partition1:scatter": "k_scatter<SrcSoAKey>",
+    kernels = {"bound": "k_bound_waves", "bound.medium": "k_bound_chunks",
+               "partition1:scatter": "k_scatter<SrcSoAKey>",
                "partition2:scatter": "k_scatter<SrcAoS>"}
     dom_stage = max(kernels, key=lambda k: stage_ms.get(k, 0.0))
     dom_kernel = kernels[dom_stage]

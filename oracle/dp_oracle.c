@@ -57,21 +57,39 @@ void dpo_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
     memcpy(out, c, sizeof(c));
 }
 
-/* pair priority: philox(seed ^ TAG_PAIR; pid, pk) */
-static inline uint32_t pair_prio(uint64_t seed, uint64_t pid, uint32_t pk) {
-    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32) ^ DPG_TAG_PAIR};
-    uint32_t c[4] = {(uint32_t)pid, pk, (uint32_t)(pid >> 32), 0u};
-    philox4x32_10(c, key);
-    return c[0];
+/* Sampling priorities (DESIGN.md "Randomness"): keyed murmur3-finalizer
+ * chains, identical to pid_hash / pair_prio_h / rec_prio_h of
+ * pipelinedp_amd/csrc/dpg_common.h.  They stand in for the reference's
+ * uniform sampling without replacement (pipeline_backend.py:531-547,
+ * sampling_utils.py:19-29): keeping the k smallest priorities of a group is
+ * a uniform k-subset; the chi-square fixture pins that distribution. */
+static inline uint32_t fmix32(uint32_t h) {
+    h ^= h >> 16;
+    h *= 0x85EBCA6Bu;
+    h ^= h >> 13;
+    h *= 0xC2B2AE35u;
+    h ^= h >> 16;
+    return h;
 }
 
-/* record priority: philox(seed ^ TAG_REC; pid, pk, global record id) */
+static inline uint32_t pid_hash(uint64_t seed, uint64_t pid) {
+    uint32_t h = fmix32((uint32_t)seed ^ DPG_TAG_PAIR ^ (uint32_t)pid);
+    return fmix32(h ^ (uint32_t)(pid >> 32) ^ (uint32_t)(seed >> 32));
+}
+
+/* pair priority (mpc sampler key) */
+static inline uint32_t pair_prio(uint64_t seed, uint64_t pid, uint32_t pk) {
+    return fmix32(pid_hash(seed, pid) ^ pk);
+}
+
+/* record priority (mcpp / L sampler key): hash << 32 | low 32 bits of the
+ * global record id */
 static inline uint64_t rec_prio(uint64_t seed, uint64_t pid, uint32_t pk, uint64_t gidx) {
-    uint32_t key[2] = {(uint32_t)seed ^ ((uint32_t)(pid >> 32) * 0x9E3779B9u),
-                       (uint32_t)(seed >> 32) ^ DPG_TAG_REC};
-    uint32_t c[4] = {(uint32_t)pid, pk, (uint32_t)gidx, (uint32_t)(gidx >> 32)};
-    philox4x32_10(c, key);
-    return ((uint64_t)c[0] << 32) | c[1];
+    uint32_t h = fmix32(pid_hash(seed, pid) ^ DPG_TAG_REC);
+    h = fmix32(h ^ pk);
+    h = fmix32(h + (uint32_t)gidx);
+    h = fmix32(h ^ (uint32_t)(gidx >> 32));
+    return ((uint64_t)h << 32) | (uint32_t)gidx;
 }
 
 static inline double u53(uint32_t a, uint32_t b) {

@@ -28,12 +28,13 @@
 #include "dpg_common.h"
 #include "dpg_partition.h"
 #include "dpg_select.h"
+#include "dpg_wave.h"
 
 using namespace dpg;
 
 namespace {
 
-constexpr uint32_t kBucketTarget = 512;  // average records per fine bucket
+constexpr uint32_t kBucketTarget = 256;  // average records per fine bucket
 constexpr uint32_t kMaxB1 = 11, kMaxB2 = 11;
 constexpr uint32_t kChunkGroup = 32;     // fine buckets per packing thread
 
@@ -50,7 +51,7 @@ struct Control {  // device-side counters, zeroed per call
     uint32_t n_chunks;
     uint32_t n_over;   // fine buckets over the chunk capacity
     uint32_t n_over2;  // refined buckets still over it
-    uint32_t pad0;
+    uint32_t n_mchunks;  // single-bucket chunks above the small-chunk capacity
     unsigned long long over_records;
     unsigned long long over2_records;
     unsigned long long pid_lo, pid_hi;  // order-preserving (x ^ 2^63) min / max
@@ -257,7 +258,7 @@ BoundParams to_bound(const dpg_bound_params *p, uint64_t seed) {
 
 struct Plan {
     uint32_t b1, b2, kbits, pkbits;
-    uint32_t plb;  // pid hash bits left below the fine buckets (<= 10)
+    uint32_t plb;  // pid hash bits left below the fine buckets (<= 7)
     int64_t P;
 };
 
@@ -268,11 +269,17 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
                      const BoundParams &bp, int64_t n, const dpg_partials *out, Control *ctl) {
     int st = DPG_OK;
     using CL = ChunkLayout<KeyT, Item>;
-    const uint32_t cap = std::min<uint32_t>(ctx->bucket_cap, (uint32_t)kBCap);
+    using WL = WaveLayout<KeyT, Item>;
+    const uint32_t capM = std::min<uint32_t>(ctx->bucket_cap, (uint32_t)kBCap);
+    // small chunks need <= 7 pid hash bits below a bucket (kWCq = 128 slots)
+    auto cap_small = [&](uint32_t plb) {
+        return plb <= 7 ? std::min<uint32_t>(capM, (uint32_t)kWCap) : 0u;
+    };
     const Fmt f = bp.fmt;
     // ---- pack fine buckets into chunks (groups never span level-1 buckets)
     stage(ctx, s, "chunks");
     WS(chunks, uint4, "chunks", B);
+    WS(mchunks, uint4, "mchunks", B);
     WS(ostart, int64_t, "over.start", B);
     WS(ocnt, uint32_t, "over.cnt", B);
     WS(od1, uint32_t, "over.d1", B);
@@ -280,8 +287,9 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     const uint32_t group = std::min<uint32_t>(kChunkGroup, 1u << pl.b2);
     const uint32_t ngroups = (B + group - 1) / group;
     k_make_chunks<<<(ngroups + 255) / 256, 256, 0, s>>>(
-        bstart, bcnt, B, group, cap, 0u, pl.b2, nullptr, nullptr, pl.plb, chunks,
-        &ctl->n_chunks, ostart, ocnt, od1, ohb, &ctl->n_over, &ctl->over_records);
+        bstart, bcnt, B, group, cap_small(pl.plb), capM, 0u, pl.b2, nullptr, nullptr, pl.plb,
+        chunks, &ctl->n_chunks, mchunks, &ctl->n_mchunks, ostart, ocnt, od1, ohb, &ctl->n_over,
+        &ctl->over_records);
     LAUNCH_CHECK();
     Control hctl;
     HIP_TRY(hipMemcpyAsync(&hctl, ctl, sizeof(Control), hipMemcpyDeviceToHost, s));
@@ -290,6 +298,7 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
         return fail(ctx, DPG_ERR_KEY_RANGE,
                     "privacy id outside its declared range or partition key outside [0, P)");
     const uint4 *chunk_list = chunks;
+    const uint4 *mchunk_list = mchunks;
     const R *refined = recs;
     // global-memory leftovers: (buffer, starts, counts, level-1 buckets, number)
     const R *g_base = recs;
@@ -323,19 +332,27 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
             if (r) return r;
             const uint32_t B2 = no * F2;
             WS(chunks2, uint4, "chunks.r", (size_t)hctl.n_chunks + B2);
-            HIP_TRY(hipMemcpyAsync(chunks2, chunks, (size_t)hctl.n_chunks * sizeof(uint4),
-                                   hipMemcpyDeviceToDevice, s));
+            WS(mchunks2, uint4, "mchunks.r", (size_t)hctl.n_mchunks + B2);
+            if (hctl.n_chunks)
+                HIP_TRY(hipMemcpyAsync(chunks2, chunks, (size_t)hctl.n_chunks * sizeof(uint4),
+                                       hipMemcpyDeviceToDevice, s));
+            if (hctl.n_mchunks)
+                HIP_TRY(hipMemcpyAsync(mchunks2, mchunks, (size_t)hctl.n_mchunks * sizeof(uint4),
+                                       hipMemcpyDeviceToDevice, s));
             WS(o2start, int64_t, "over2.start", B2);
             WS(o2cnt, uint32_t, "over2.cnt", B2);
             WS(o2d1, uint32_t, "over2.d1", B2);
             WS(o2hb, uint32_t, "over2.hb", B2);
+            const uint32_t plb2 = pl.plb - rbits;
             k_make_chunks<<<(no + 255) / 256, 256, 0, s>>>(
-                base2, tot2, B2, F2, cap, 1u, rbits, od1, ohb, pl.plb - rbits, chunks2,
-                &ctl->n_chunks, o2start, o2cnt, o2d1, o2hb, &ctl->n_over2, &ctl->over2_records);
+                base2, tot2, B2, F2, cap_small(plb2), capM, 1u, rbits, od1, ohb, plb2, chunks2,
+                &ctl->n_chunks, mchunks2, &ctl->n_mchunks, o2start, o2cnt, o2d1, o2hb,
+                &ctl->n_over2, &ctl->over2_records);
             LAUNCH_CHECK();
             HIP_TRY(hipMemcpyAsync(&hctl, ctl, sizeof(Control), hipMemcpyDeviceToHost, s));
             HIP_TRY(hipStreamSynchronize(s));
             chunk_list = chunks2;
+            mchunk_list = mchunks2;
             refined = rbuf;
             g_base = rbuf;
             g_start = o2start;
@@ -344,16 +361,33 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
             n_global = hctl.n_over2;
         }
     }
-    // ---- bounding of every chunk in LDS; workgroup g writes its items to
-    // items[wg_off[g], ...), the global-memory path after all of them
-    const uint32_t G = (uint32_t)std::min(ctx->n_cu * CL::PER_CU, 1022);
+    // ---- bounding in LDS: Gw single-wave workgroups over the small chunks,
+    // Gm 256-thread workgroups over the medium ones (launched only if there
+    // are any), the global-memory path last; workgroup g of the Gw + Gm + 1
+    // writes its items to items[wg_off[g], ...)
+    // resident single-wave workgroups per CU: the LDS share or the register
+    // file, whichever binds (a static schedule must not oversubscribe)
+    int wpc = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&wpc, k_bound_waves<KeyT, Item, R>, 64,
+                                                     WL::TOTAL) != hipSuccess ||
+        wpc <= 0)
+        wpc = 1;
+    const uint32_t Gw = (uint32_t)(ctx->n_cu * std::min(wpc, WL::PER_CU));
+    const uint32_t Gm = hctl.n_mchunks ? (uint32_t)std::min<uint32_t>(
+                                             ctx->n_cu * CL::PER_CU, hctl.n_mchunks)
+                                       : 0u;
+    const uint32_t G = Gw + Gm;
     WS(items, Item, "items", std::max<int64_t>(n, 1));
     WS(wg_rec, uint32_t, "wg.rec", G + 1);
     WS(wg_off, int64_t, "wg.off", G + 2);
     WS(wg_cnt, uint32_t, "wg.cnt", G + 1);
     WS(wg_pre, int64_t, "wg.pre", G + 2);
-    k_wg_records<<<G, 256, 0, s>>>(chunk_list, &ctl->n_chunks, G, wg_rec);
+    k_wg_records<<<Gw, 256, 0, s>>>(chunk_list, &ctl->n_chunks, Gw, wg_rec);
     LAUNCH_CHECK();
+    if (Gm) {
+        k_wg_records<<<Gm, 256, 0, s>>>(mchunk_list, &ctl->n_mchunks, Gm, wg_rec + Gw);
+        LAUNCH_CHECK();
+    }
     k_scan_small<<<1, 1024, 0, s>>>(wg_rec, G, wg_off, nullptr);
     LAUNCH_CHECK();
     HIP_TRY(hipMemsetAsync(wg_cnt + G, 0, 4, s));
@@ -363,32 +397,53 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     const bool timing = std::getenv("DPG_PHASE_TIMING") != nullptr;
     bpl.phase_cyc = nullptr;
     if (timing) {
-        WS(pc, unsigned long long, "bound.phase_cyc", 16);
-        HIP_TRY(hipMemsetAsync(pc, 0, 16 * 8, s));
+        WS(pc, unsigned long long, "bound.phase_cyc", 32);
+        HIP_TRY(hipMemsetAsync(pc, 0, 32 * 8, s));
         bpl.phase_cyc = pc;
     }
-    (void)hipFuncSetAttribute((const void *)k_bound_chunks<KeyT, Item, R>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)CL::TOTAL);
+    (void)hipFuncSetAttribute((const void *)k_bound_waves<KeyT, Item, R>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)WL::TOTAL);
     stage(ctx, s, "bound");
-    k_bound_chunks<KeyT, Item, R><<<G, kBT, CL::TOTAL, s>>>(recs, refined, chunk_list,
-                                                           &ctl->n_chunks, bpl, items, wg_off,
-                                                           wg_cnt);
+    k_bound_waves<KeyT, Item, R><<<Gw, 64, WL::TOTAL, s>>>(recs, refined, chunk_list,
+                                                          &ctl->n_chunks, bpl, items, wg_off,
+                                                          wg_cnt);
     LAUNCH_CHECK();
+    if (prog) watchdog_wait(s, prog, Gw, "k_bound_waves");
+    stage(ctx, s, "bound.medium");
+    if (Gm) {
+        BoundParams bpm = bpl;
+        if (timing) bpm.phase_cyc = bpl.phase_cyc + 16;
+        if (prog) bpm.progress = prog + Gw;
+        (void)hipFuncSetAttribute((const void *)k_bound_chunks<KeyT, Item, R>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)CL::TOTAL);
+        k_bound_chunks<KeyT, Item, R><<<Gm, kBT, CL::TOTAL, s>>>(
+            recs, refined, mchunk_list, &ctl->n_mchunks, bpm, items, wg_off + Gw, wg_cnt + Gw);
+        LAUNCH_CHECK();
+        if (prog) watchdog_wait(s, prog + Gw, Gm, "k_bound_chunks");
+    }
     stage(ctx, s, "bound.tail");
-    if (prog) watchdog_wait(s, prog, G, "k_bound_chunks");
     if (timing) {
-        unsigned long long h[16];
+        unsigned long long h[32];
         HIP_TRY(hipMemcpy(h, bpl.phase_cyc, sizeof(h), hipMemcpyDeviceToHost));
-        static const char *nm[9] = {"A0.cas", "A1.count", "A2.barrier", "B.slots", "C.mpc",
-                                    "D.state", "E.mcpp", "F.acc", "G.emit"};
-        unsigned long long tot = 0;
-        for (int i = 0; i <= 8; ++i) tot += h[i];
-        std::fprintf(stderr, "[dpg phase] chunks=%u over=%u over2=%u per-WG Mcycles:",
-                     hctl.n_chunks, hctl.n_over, hctl.n_over2);
-        for (int i = 0; i <= 8; ++i)
-            std::fprintf(stderr, " %s=%.3f(%.0f%%)", nm[i], h[i] / 1e6 / G,
-                         100.0 * h[i] / (tot ? tot : 1));
-        std::fprintf(stderr, "\n");
+        static const char *nmw[10] = {"A0.cas", "A1.count", "B.slots", "C1.cand", "C2.rank",
+                                      "D.state", "E.mcpp", "F.acc", "G.emit", "A.probe"};
+        static const char *nmc[9] = {"A0.cas", "A1.count", "A2.barrier", "B.slots", "C.mpc",
+                                     "D.state", "E.mcpp", "F.acc", "G.emit"};
+        for (int part = 0; part < 2; ++part) {
+            const unsigned long long *hp = h + 16 * part;
+            const uint32_t gg = part ? Gm : Gw;
+            if (!gg) continue;
+            unsigned long long tot = 0;
+            const int np = part ? 9 : 10;
+            for (int i = 0; i < np; ++i) tot += hp[i];
+            std::fprintf(stderr, "[dpg phase] %s chunks=%u over=%u over2=%u per-WG Mcycles:",
+                         part ? "medium" : "small", part ? hctl.n_mchunks : hctl.n_chunks,
+                         hctl.n_over, hctl.n_over2);
+            for (int i = 0; i < np; ++i)
+                std::fprintf(stderr, " %s=%.3f(%.0f%%)", (part ? nmc : nmw)[i], hp[i] / 1e6 / gg,
+                             100.0 * hp[i] / (tot ? tot : 1));
+            std::fprintf(stderr, "\n");
+        }
     }
     // ---- single buckets beyond the chunk capacity: global-memory working sets
     if (n_global > 0) {
@@ -625,10 +680,10 @@ int dpg_bound_aggregate(dpg_ctx *ctx, const int64_t *pid, const int64_t *pk, con
     pl.kbits = std::max<uint32_t>(1, bits_for(U));
     pl.pkbits = std::max<uint32_t>(1, bits_for((uint64_t)P));
     const uint32_t target = ctx->bucket_target ? ctx->bucket_target : kBucketTarget;
-    // at most 10 pid hash bits may stay below a fine bucket (direct pid slots
-    // in the bound kernel), hence the lower bound kbits - 10
+    // at most 7 pid hash bits may stay below a fine bucket (direct pid slots
+    // of a small chunk: kWCq = 128), hence the lower bound kbits - 7
     uint32_t bits_total = bits_for((uint64_t)((n + target - 1) / target));
-    bits_total = std::max<uint32_t>(bits_total, pl.kbits > 10 ? pl.kbits - 10 : 0);
+    bits_total = std::max<uint32_t>(bits_total, pl.kbits > 7 ? pl.kbits - 7 : 0);
     bits_total = std::max<uint32_t>(1, std::min<uint32_t>(bits_total, kMaxB1 + kMaxB2));
     bits_total = std::min<uint32_t>(bits_total, pl.kbits);
     // one level up to 11 bits; beyond, the smaller half first (level 1 reads

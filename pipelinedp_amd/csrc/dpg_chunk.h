@@ -33,6 +33,16 @@ constexpr uint32_t kMcppBase = 1024;
 constexpr int kQPT = kCq / kBT;      // pid slots per thread
 constexpr int kPPT = kCp / kBT;      // pair slots per thread
 
+// small chunks: one wave each (dpg_wave.h)
+constexpr int kWCap = 512;             // records per small chunk
+constexpr int kWRPT = kWCap / 64;      // records per lane
+constexpr uint32_t kWCq = 128;         // direct pid slots per small chunk
+constexpr uint32_t kWCp = 512;         // pairs (dense ids) per small chunk
+constexpr uint32_t kWCk = 1024;        // pair key table slots (load <= 1/2)
+constexpr uint32_t kWPool = 512;       // selection keys (mpc regions, then mcpp regions)
+constexpr int kWQPL = kWCq / 64;       // pid slots per lane
+constexpr int kWPPL = kWCp / 64;       // pair slots per lane
+
 struct ChunkShared {
     uint32_t bump, bump2, nitems, npair, npid, pad[3];
 };
@@ -609,55 +619,67 @@ __global__ __launch_bounds__(256) void k_wg_records(const uint4 *chunks, const u
     if (threadIdx.x == 0) wg_rec[g] = part[0] + part[1] + part[2] + part[3];
 }
 
-// out[i] = sum(in[0, i)) for i <= m (m < 1024); optionally *total32 = out[m]
+// out[i] = sum(in[0, i)) for i <= m (one workgroup, 1024 entries per round);
+// optionally *total32 = out[m]
 __global__ __launch_bounds__(1024) void k_scan_small(const uint32_t *in, uint32_t m, int64_t *out,
                                                      uint32_t *total32) {
     __shared__ int64_t sh[1024];
+    __shared__ int64_t carry;
     const uint32_t t = threadIdx.x;
-    sh[t] = t < m ? (int64_t)in[t] : 0;
+    if (t == 0) carry = 0;
     __syncthreads();
-    for (uint32_t o = 1; o < 1024; o <<= 1) {
-        int64_t x = t >= o ? sh[t - o] : 0;
+    for (uint32_t b = 0; b <= m; b += 1024) {
+        const uint32_t i = b + t;
+        sh[t] = i < m ? (int64_t)in[i] : 0;
         __syncthreads();
-        sh[t] += x;
+        for (uint32_t o = 1; o < 1024; o <<= 1) {
+            int64_t x = t >= o ? sh[t - o] : 0;
+            __syncthreads();
+            sh[t] += x;
+            __syncthreads();
+        }
+        if (i <= m) out[i] = carry + (t ? sh[t - 1] : 0);
+        __syncthreads();
+        if (t == 0) carry += sh[1023];
         __syncthreads();
     }
-    if (t <= m) out[t] = t ? sh[t - 1] : 0;
-    if (t == 0 && total32) *total32 = m ? (uint32_t)sh[m - 1] : 0u;
+    if (t == 0 && total32) *total32 = (uint32_t)carry;
 }
 
-// Greedy packing of consecutive fine buckets into chunks of <= cap records,
-// one thread per group of `group` buckets; a group never spans two level-1
-// buckets: bucket b belongs to level-1 bucket b >> d1_shift (group divides
-// 1 << d1_shift), or to d1_map[b >> d1_shift] for refined buckets.  A
-// bucket's pid hash-residual base is (b mod 2^d1_shift) << plb (plus
-// hb_map[b >> d1_shift] for refined buckets); a chunk spans at most
-// kCq >> plb bucket indices, so its pid slots (residual - chunk base) stay
-// below kCq.  Buckets larger than cap go to the oversize list (start, count,
-// level-1 bucket, residual base).  sel = buffer the buckets live in.
+// Greedy packing of consecutive fine buckets into small chunks of <= capS
+// records (single-wave kernel, dpg_wave.h), one thread per group of `group`
+// buckets; a group never spans two level-1 buckets: bucket b belongs to
+// level-1 bucket b >> d1_shift (group divides 1 << d1_shift), or to
+// d1_map[b >> d1_shift] for refined buckets.  A bucket's pid hash-residual
+// base is (b mod 2^d1_shift) << plb (plus hb_map[b >> d1_shift] for refined
+// buckets); a small chunk spans at most kWCq >> plb bucket indices, so its
+// pid slots (residual - chunk base) stay below kWCq.  Buckets of (capS, capM]
+// records become single-bucket medium chunks (workgroup kernel above), larger
+// ones go to the oversize list (start, count, level-1 bucket, residual base).
+// sel = buffer the buckets live in.
 __global__ void k_make_chunks(const int64_t *bstart, const uint32_t *bcnt, uint32_t B,
-                              uint32_t group, uint32_t cap, uint32_t sel, uint32_t d1_shift,
-                              const uint32_t *d1_map, const uint32_t *hb_map, uint32_t plb,
-                              uint4 *chunks, uint32_t *n_chunks, int64_t *over_start,
-                              uint32_t *over_cnt, uint32_t *over_d1, uint32_t *over_hb,
-                              uint32_t *n_over, unsigned long long *over_records) {
+                              uint32_t group, uint32_t capS, uint32_t capM, uint32_t sel,
+                              uint32_t d1_shift, const uint32_t *d1_map, const uint32_t *hb_map,
+                              uint32_t plb, uint4 *chunks, uint32_t *n_chunks, uint4 *mchunks,
+                              uint32_t *n_mchunks, int64_t *over_start, uint32_t *over_cnt,
+                              uint32_t *over_d1, uint32_t *over_hb, uint32_t *n_over,
+                              unsigned long long *over_records) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t b0 = g * group;
     if (b0 >= B) return;
     const uint32_t b1 = min(B, b0 + group);
-    const uint32_t maxspan = kCq >> plb;
+    const uint32_t maxspan = max(1u, kWCq >> plb);
     const uint32_t lmask = (1u << d1_shift) - 1u;
     const uint32_t d1 = d1_map ? d1_map[b0 >> d1_shift] : (b0 >> d1_shift);
     const uint32_t hb0 = hb_map ? hb_map[b0 >> d1_shift] : 0u;
-    // pass 1: count chunks
+    // pass 1: count small chunks
     uint32_t nc = 0, cur = 0, bfirst = 0;
     int64_t cend = -1;
     for (uint32_t b = b0; b < b1; ++b) {
         const uint32_t c = bcnt[b];
-        if (c == 0) continue;
-        if (c > cap) continue;
+        if (c == 0 || c > capS) continue;
         const int64_t st = bstart[b];
-        if (cur == 0 || cur + c > cap || st != cend || b - bfirst >= maxspan) {
+        if (cur == 0 || cur + c > capS || st != cend || b - bfirst >= maxspan) {
             ++nc;
             cur = 0;
             bfirst = b;
@@ -676,7 +698,7 @@ __global__ void k_make_chunks(const int64_t *bstart, const uint32_t *bcnt, uint3
         if (c == 0) continue;
         const int64_t st = bstart[b];
         const uint32_t hb = hb0 + ((b & lmask) << plb);
-        if (c > cap) {
+        if (c > capM) {
             const uint32_t o = atomicAdd(n_over, 1u);
             over_start[o] = st;
             over_cnt[o] = c;
@@ -685,7 +707,11 @@ __global__ void k_make_chunks(const int64_t *bstart, const uint32_t *bcnt, uint3
             atomicAdd(over_records, (unsigned long long)c);
             continue;
         }
-        if (cur == 0 || cur + c > cap || st != cend || b - bfirst >= maxspan) {
+        if (c > capS) {
+            mchunks[atomicAdd(n_mchunks, 1u)] = make_uint4((uint32_t)st, c | (sel << 31), d1, hb);
+            continue;
+        }
+        if (cur == 0 || cur + c > capS || st != cend || b - bfirst >= maxspan) {
             if (cur)
                 chunks[base++] = make_uint4((uint32_t)cst, cur | (sel << 31), d1,
                                             hb0 + ((bfirst & lmask) << plb));

@@ -164,21 +164,33 @@ __host__ __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
     return h;
 }
 
-// Pair priority: philox(seed ^ TAG_PAIR; pid, pk) -- the mpc sampler key.
-__device__ __forceinline__ uint32_t pair_prio(uint64_t seed, uint64_t pid, uint32_t pk) {
-    uint32_t c[4] = {(uint32_t)pid, pk, (uint32_t)(pid >> 32), 0u};
-    philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32) ^ DPG_TAG_PAIR);
-    return c[0];
+// Sampling priorities (DESIGN.md "Randomness"): keyed chains of the murmur3
+// finalizer.  Sampling only has to be uniform without replacement -- the
+// privacy guarantee holds for any choice of kept records -- so a cheap mixer
+// replaces Philox here (noise keeps Philox).  pid_hash is the per-privacy-id
+// state (computed once per pid in the bound kernels); pair_prio_h orders the
+// pid's partitions (mpc), rec_prio_h the records of a pair or pid (mcpp, L)
+// with the low 32 bits of the global record id as tie-break.
+__host__ __device__ __forceinline__ uint32_t pid_hash(uint64_t seed, uint64_t pid) {
+    const uint32_t h = fmix32((uint32_t)seed ^ DPG_TAG_PAIR ^ (uint32_t)pid);
+    return fmix32(h ^ (uint32_t)(pid >> 32) ^ (uint32_t)(seed >> 32));
 }
-
-// Record priority: philox(seed ^ TAG_REC; pid, pk, global record id) -- the
-// mcpp / L1 sampler key.
+__host__ __device__ __forceinline__ uint32_t pair_prio_h(uint32_t hp, uint32_t pk) {
+    return fmix32(hp ^ pk);
+}
+__host__ __device__ __forceinline__ uint64_t rec_prio_h(uint32_t hp, uint32_t pk, uint64_t gidx) {
+    uint32_t h = fmix32(hp ^ DPG_TAG_REC);
+    h = fmix32(h ^ pk);
+    h = fmix32(h + (uint32_t)gidx);
+    h = fmix32(h ^ (uint32_t)(gidx >> 32));
+    return ((uint64_t)h << 32) | (uint32_t)gidx;
+}
+__device__ __forceinline__ uint32_t pair_prio(uint64_t seed, uint64_t pid, uint32_t pk) {
+    return pair_prio_h(pid_hash(seed, pid), pk);
+}
 __device__ __forceinline__ uint64_t rec_prio(uint64_t seed, uint64_t pid, uint32_t pk,
                                              uint64_t gidx) {
-    uint32_t c[4] = {(uint32_t)pid, pk, (uint32_t)gidx, (uint32_t)(gidx >> 32)};
-    philox4x32_10(c, (uint32_t)seed ^ ((uint32_t)(pid >> 32) * 0x9E3779B9u),
-                  (uint32_t)(seed >> 32) ^ DPG_TAG_REC);
-    return ((uint64_t)c[0] << 32) | c[1];
+    return rec_prio_h(pid_hash(seed, pid), pk, gidx);
 }
 
 __device__ __forceinline__ double u53(uint32_t a, uint32_t b) {

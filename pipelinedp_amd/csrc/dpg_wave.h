@@ -1,0 +1,699 @@
+// dpg_wave.h -- contribution bounding of small chunks by single waves (gfx950).
+//
+// The hot path of the bound stage.  Every 64-lane workgroup is one wave that
+// owns a private ~17 KB LDS working set and walks its share of the chunk list
+// (chunks of <= kWCap = 512 records: the fine buckets of the partition
+// levels, packed).  Nothing is shared between waves, so there is no
+// workgroup barrier at all: phases are ordered by the wave's own program
+// order (LDS instructions of one wave execute in order; a wavefront fence
+// keeps the compiler from reordering them), counters live in scalar
+// registers and allocations are ballot + mbcnt instead of LDS atomics.
+// Nine such waves share a CU, so one wave's LDS round trips overlap the
+// others' work.
+//
+// Per chunk (same algorithm as dpg_bound.h / dpg_chunk.h, identical results):
+//   A  pair inserts (pid slot = pid hash residual - chunk base: direct, no
+//      table), counts, dense pair / pid lists, pid values
+//   B  every pid over its limit reserves one pool slot per pair (record in
+//      PER_PRIVACY_ID mode)
+//   C  mpc selection: candidates (priority below a per-pid threshold) append
+//      their pair key to the pid's pool region and are kept iff fewer than
+//      mpc candidates have a smaller key; pids short of candidates rank their
+//      non-candidates too (rare)          (contribution_bounders.py:90-92)
+//   D  pair state; over-full kept pairs reserve one pool slot per record
+//   E  their records append philox(seed, pid, pk, record id) keys; values of
+//      records of kept pairs are gathered by record index
+//   F  a sampled record is kept iff fewer than mcpp keys of its pair are
+//      smaller (:74-76); clipped accumulators (combiners.py:255-500)
+//   G  emit one Item per kept pair; clear the occupied slots
+#pragma once
+
+#include "dpg_chunk.h"
+
+namespace dpg {
+
+
+template <class KeyT, class Item>
+struct WaveLayout {
+    static constexpr bool var = ItemTraits<Item>::var;
+    static constexpr size_t PIDV = 0;                   // pid_hash of the privacy id
+    static constexpr size_t PIDM = PIDV + 4 * kWCq;     // low 16: pairs/records, high: appends
+    static constexpr size_t PIDSLOT = PIDM + 4 * kWCq;  // pool base (+ appends << 16) or kNil
+    static constexpr size_t QLIST = PIDSLOT + 4 * kWCq;
+    // pair key table (kWCk slots); once every insert has settled, a slot
+    // holds its pair's dense id instead of the key
+    static constexpr size_t KEYS = QLIST + 2 * kWCq;
+    static constexpr size_t PKEY = KEYS + sizeof(KeyT) * kWCk;  // dense: pair key
+    static constexpr size_t PCNT = PKEY + sizeof(KeyT) * kWCp;  // dense: records
+    static constexpr size_t PST = PCNT + 4 * kWCp;              // dense: state
+    static constexpr size_t POOL = PST + 4 * kWCp;
+    static constexpr size_t ACC = POOL + 8 * kWPool;
+    static constexpr size_t SH = ACC + 8 * kWCp * (var ? 3 : 1);
+    // padded to a multiple of 4 KB so that the allocation granularity of LDS
+    // cannot cost a resident wave (20 KB: 8 per CU)
+    static constexpr size_t TOTAL = (SH + 16 + 4095) & ~(size_t)4095;
+    static constexpr int PER_CU = (int)((160 * 1024) / TOTAL) < 16 ? (int)((160 * 1024) / TOTAL) : 16;
+    static_assert(TOTAL <= 40 * 1024, "wave working set too large");
+    static_assert(8 * kWPool >= sizeof(KeyT) * kWCap, "pool hosts the dummy CAS words");
+    static_assert(KEYS % 16 == 0, "key table cleared by 16-byte stores");
+};
+
+// Compiler-level ordering of one wave's LDS accesses between phases (the
+// hardware already executes them in order).
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Count of keys in a[base, base + cnt) below x for every slot j with
+// cnt[j] > 0, batched across the slots: every round issues W clamped loads
+// per slot before any compare, so the LDS round trips of all slots overlap.
+// Slots j >= jn (uniform) hold nothing and are skipped.
+template <int J, int W = 2>
+__device__ __forceinline__ void rank_batch(const uint64_t *pool, const uint32_t (&base)[J],
+                                           const uint32_t (&cnt)[J], const uint64_t (&x)[J],
+                                           uint32_t (&rk)[J], uint32_t jn) {
+    uint32_t mx = 0;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        rk[j] = 0;
+        if (j < jn) mx = max(mx, cnt[j]);
+    }
+    for (uint32_t t = 0; __ballot(t < mx); t += W) {
+        uint64_t y[J][W];
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            if (j >= jn) continue;
+            const uint32_t last = cnt[j] ? cnt[j] - 1 : 0;
+#pragma unroll
+            for (int u = 0; u < W; ++u) y[j][u] = pool[base[j] + min(t + u, last)];
+        }
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            if (j >= jn) continue;
+#pragma unroll
+            for (int u = 0; u < W; ++u) rk[j] += (t + u < cnt[j] && y[j][u] < x[j]) ? 1u : 0u;
+        }
+    }
+}
+
+// Records past the chunk end hold a copy of its last record (loads are
+// unconditional); they aim their table CAS at lane-private dummy words and
+// take part in nothing that counts.  Every phase is written stage-wise over
+// the lane's kWRPT records / kWPPL pairs (all loads of a stage issued before
+// any use), so one wave keeps many LDS round trips in flight.  Pairs get
+// dense ids 0..npair-1 when they are created; every per-pair array is dense.
+template <class KeyT, class Item, class R>
+__device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, uint32_t d1,
+                                               uint32_t hbase, char *smem, const BoundParams &bp,
+                                               Item *items, uint32_t nitems, PhaseTimer &clk) {
+    using L = WaveLayout<KeyT, Item>;
+    constexpr bool kVar = L::var;
+    uint32_t *pidv = reinterpret_cast<uint32_t *>(smem + L::PIDV);
+    uint32_t *pidm = reinterpret_cast<uint32_t *>(smem + L::PIDM);
+    uint32_t *pidslot = reinterpret_cast<uint32_t *>(smem + L::PIDSLOT);
+    uint16_t *qlist = reinterpret_cast<uint16_t *>(smem + L::QLIST);
+    KeyT *keys = reinterpret_cast<KeyT *>(smem + L::KEYS);
+    KeyT *pkey_d = reinterpret_cast<KeyT *>(smem + L::PKEY);
+    uint32_t *pcnt = reinterpret_cast<uint32_t *>(smem + L::PCNT);
+    uint32_t *pst = reinterpret_cast<uint32_t *>(smem + L::PST);
+    uint64_t *pool = reinterpret_cast<uint64_t *>(smem + L::POOL);
+    double *acc_sum = reinterpret_cast<double *>(smem + L::ACC);
+    double *acc_nsum = acc_sum + kWCp;
+    double *acc_nsq = acc_nsum + kWCp;
+    uint32_t *bump = reinterpret_cast<uint32_t *>(smem + L::SH);
+
+    const uint32_t lane = __lane_id();
+    const Fmt f = bp.fmt;
+    const uint32_t pkb = f.pkbits;
+    const uint64_t pkmask = (1ull << pkb) - 1ull;
+    const bool per_pid = bp.mode == DPG_MODE_PER_PRIVACY_ID;
+    const bool need_v = bp.need_values != 0;
+    const bool sample = bp.mode == DPG_MODE_CROSS_AND_PER_PARTITION && need_v;
+    const bool part_clip = bp.sum_mode == DPG_SUM_CLIP_PARTITION;
+    const uint32_t lim = per_pid ? bp.L : bp.mpc;
+    const uint32_t hshift = f.kbits - f.b1;
+    const uint32_t kn = (n + 63) >> 6;  // occupied record slots per lane (uniform)
+
+    // ---- A: pair inserts: home-slot CAS of all records in flight, then
+    // linear probing of the colliding ones, one probe step of all of them per
+    // round (table load <= 1/2)
+    uint32_t qs[kWRPT], dn[kWRPT];
+    uint32_t validm = 0;  // per-lane bit k
+    uint32_t npair = 0, npid = 0;
+    {
+        uint32_t ps[kWRPT], wonm = 0;
+        KeyT pkey[kWRPT], op[kWRPT];
+#pragma unroll
+        for (int k = 0; k < kWRPT; ++k) {
+            const bool valid = lane + 64u * k < n;
+            validm |= valid ? 1u << k : 0u;
+            const uint64_t key = RecOps<R>::key(r[k], f);
+            qs[k] = ((uint32_t)(key >> pkb) - hbase) & (kWCq - 1);
+            pkey[k] = ((KeyT)qs[k] << pkb) | (KeyT)(key & pkmask);
+            ps[k] = hslot(pkey[k], kWCk - 1);
+            KeyT *tgt = valid ? keys + ps[k] : reinterpret_cast<KeyT *>(pool) + (lane + 64u * k);
+            op[k] = cas_home<KeyT>(tgt, 0, pkey[k]);
+        }
+        mark(bp, 0, clk);
+        uint32_t pend = 0;
+#pragma unroll
+        for (int k = 0; k < kWRPT; ++k) {
+            if (!((validm >> k) & 1u)) continue;
+            if (op[k] == empty_key<KeyT>()) wonm |= 1u << k;
+            else if (op[k] != pkey[k]) pend |= 1u << k;
+        }
+        for (uint32_t it = 0; __ballot(pend != 0); ++it) {
+            if (it >= kWCk) {
+                if (pend) atomicOr(bp.err, 2u);
+                break;
+            }
+#pragma unroll
+            for (int k = 0; k < kWRPT; ++k) {
+                if ((pend >> k) & 1u) {
+                    ps[k] = (ps[k] + 1) & (kWCk - 1);
+                    op[k] = cas_home<KeyT>(keys, ps[k], pkey[k]);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < kWRPT; ++k) {
+                if ((pend >> k) & 1u) {
+                    if (op[k] == empty_key<KeyT>()) {
+                        wonm |= 1u << k;
+                        pend &= ~(1u << k);
+                    } else if (op[k] == pkey[k]) {
+                        pend &= ~(1u << k);
+                    }
+                }
+            }
+        }
+        mark(bp, 9, clk);
+        // winners: dense pair ids (the probing is over: slots now hold ids)
+#pragma unroll
+        for (int k = 0; k < kWRPT; ++k) {
+            const bool won = (wonm >> k) & 1u;
+            const uint64_t bw = __ballot(won);
+            if (won) {
+                const uint32_t d = npair + lanes_below(bw);
+                keys[ps[k]] = (KeyT)d;
+                pkey_d[d] = pkey[k];
+                pcnt[d] = 0;
+                if (need_v) {
+                    acc_sum[d] = 0.0;
+                    if (kVar) {
+                        acc_nsum[d] = 0.0;
+                        acc_nsq[d] = 0.0;
+                    }
+                }
+                if (per_pid) pst[d] = 0;
+            }
+            npair += (uint32_t)__popcll(bw);
+        }
+        wave_sync();
+#pragma unroll
+        for (int k = 0; k < kWRPT; ++k) dn[k] = (uint32_t)keys[ps[k]] & (kWCp - 1);
+        // counts (all in flight); the returned pid count tells the pid's
+        // first toucher (a pair's winner; any record in PER_PRIVACY_ID mode)
+        const uint32_t touchm = per_pid ? validm : wonm;
+        uint32_t oldm[kWRPT];
+#pragma unroll
+        for (int k = 0; k < kWRPT; ++k) {
+            if ((validm >> k) & 1u) atomicAdd(&pcnt[dn[k]], 1u);
+            oldm[k] = atomicAdd(&pidm[qs[k]], (touchm >> k) & 1u);
+        }
+#pragma unroll
+        for (int k = 0; k < kWRPT; ++k) {
+            const bool first = ((touchm >> k) & 1u) && oldm[k] == 0u;
+            const uint64_t bq = __ballot(first);
+            if (first) {
+                qlist[npid + lanes_below(bq)] = (uint16_t)qs[k];
+                pidv[qs[k]] = pid_hash(
+                    bp.seed,
+                    (uint64_t)(bp.pid_min + (int64_t)hk_inv((d1 << hshift) | (hbase + qs[k]), bp.hash)));
+            }
+            npid += (uint32_t)__popcll(bq);
+        }
+    }
+    if (lane == 0) {
+        bump[0] = 0;
+        bump[1] = 0;
+    }
+    const uint32_t jn = (npair + 63) >> 6;  // occupied pair slots per lane (uniform)
+    wave_sync();
+    mark(bp, 1, clk);
+    // ---- B: pool regions for pids over their limit
+    uint32_t qv[kWQPL];
+#pragma unroll
+    for (int j = 0; j < kWQPL; ++j) qv[j] = qlist[min(lane + 64u * j, npid - 1)] & (kWCq - 1);
+    {
+        uint32_t m[kWQPL];
+#pragma unroll
+        for (int j = 0; j < kWQPL; ++j) m[j] = pidm[qv[j]] & 0xFFFFu;
+#pragma unroll
+        for (int j = 0; j < kWQPL; ++j) {
+            const bool occ = lane + 64u * j < npid;
+            const bool want = occ && m[j] > lim;
+            const uint32_t sl = want ? atomicAdd(&bump[0], m[j]) : kNil;
+            if (occ) pidslot[qv[j]] = sl;
+        }
+    }
+    wave_sync();
+    mark(bp, 2, clk);
+
+    // pair-major state: pair j of this lane is dense id lane + 64 j (< npair)
+    KeyT pkv[kWPPL];
+    uint32_t keptm = 0, ecnt[kWPPL];
+#pragma unroll
+    for (int j = 0; j < kWPPL; ++j) pkv[j] = pkey_d[lane + 64u * j];
+    if (!per_pid) {
+        // ---- C1: candidates (priority below the pid's threshold) append
+        // their pair key to the pid's region
+        uint32_t sb[kWPPL], nc[kWPPL];
+        uint64_t k64[kWPPL];
+        uint32_t overm = 0, candm = 0;
+        {
+            uint32_t pv[kWPPL], m[kWPPL];
+#pragma unroll
+            for (int j = 0; j < kWPPL; ++j) {
+                const uint32_t q = (uint32_t)(pkv[j] >> pkb) & (kWCq - 1);
+                sb[j] = pidslot[q];
+                pv[j] = pidv[q];
+                m[j] = pidm[q] & 0xFFFFu;
+            }
+#pragma unroll
+            for (int j = 0; j < kWPPL; ++j) {
+                const bool occ = lane + 64u * j < npair;
+                k64[j] = 0;
+                if (occ) keptm |= 1u << j;
+                if (!occ || sb[j] == kNil) continue;
+                overm |= 1u << j;
+                const uint32_t pk = (uint32_t)(pkv[j] & (KeyT)pkmask);
+                const uint32_t pr = pair_prio_h(pv[j], pk);
+                k64[j] = ((uint64_t)pr << 32) | pk;
+                if (pr < cand_threshold(m[j], bp.mpc)) candm |= 1u << j;
+            }
+            uint32_t pos[kWPPL];
+#pragma unroll
+            for (int j = 0; j < kWPPL; ++j) {
+                const uint32_t q = (uint32_t)(pkv[j] >> pkb) & (kWCq - 1);
+                pos[j] = ((candm >> j) & 1u) ? atomicAdd(&pidm[q], 1u << 16) >> 16 : 0u;
+            }
+#pragma unroll
+            for (int j = 0; j < kWPPL; ++j)
+                if ((candm >> j) & 1u) pool[sb[j] + pos[j]] = k64[j];
+        }
+        wave_sync();
+        mark(bp, 3, clk);
+        // ---- C2: with >= mpc candidates, a candidate is kept iff fewer than
+        // mpc candidates have a smaller key; with fewer (rare), every
+        // candidate is kept and the non-candidates append after them (C3)
+        // Pid-major threshold search: for up to 4 pids at a time, lane e
+        // holds candidate e of each pid's region and counts the smaller keys
+        // (broadcast loads); the candidate of rank mpc - 1 is the pid's
+        // threshold, written over the region's first entry.
+        {
+            uint32_t psb[kWQPL], pnc[kWQPL];
+#pragma unroll
+            for (int j = 0; j < kWQPL; ++j) {
+                psb[j] = pidslot[qv[j]];
+                pnc[j] = pidm[qv[j]] >> 16;
+            }
+#pragma unroll
+            for (int j = 0; j < kWQPL; ++j) {
+                if (!(lane + 64u * j < npid && psb[j] != kNil && pnc[j] >= bp.mpc)) {
+                    psb[j] = 0;
+                    pnc[j] = 0;
+                }
+            }
+            for (uint32_t i0 = 0; i0 < npid; i0 += 4) {
+                uint32_t vs = psb[0], vn = pnc[0];
+#pragma unroll
+                for (int j = 1; j < kWQPL; ++j)
+                    if ((i0 >> 6) == (uint32_t)j) {
+                        vs = psb[j];
+                        vn = pnc[j];
+                    }
+                uint32_t sb4[4], nc4[4], mxn = 0;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    sb4[u] = __builtin_amdgcn_readlane(vs, (i0 + u) & 63);
+                    nc4[u] = i0 + u < npid ? __builtin_amdgcn_readlane(vn, (i0 + u) & 63) : 0u;
+                    mxn = max(mxn, nc4[u]);
+                }
+                if (mxn == 0) continue;
+                uint64_t T4[4] = {~0ull, ~0ull, ~0ull, ~0ull};
+                for (uint32_t l0 = 0; l0 < mxn; l0 += 64) {
+                    const uint32_t e = l0 + lane;
+                    uint64_t x[4];
+                    uint32_t rk[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        x[u] = pool[sb4[u] + min(e, nc4[u] ? nc4[u] - 1 : 0u)];
+                        rk[u] = 0;
+                    }
+                    for (uint32_t t = 0; t < mxn; t += 4) {
+                        uint64_t y[4][4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u)
+#pragma unroll
+                            for (int w = 0; w < 4; ++w)
+                                y[u][w] = pool[sb4[u] + min(t + w, nc4[u] ? nc4[u] - 1 : 0u)];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u)
+#pragma unroll
+                            for (int w = 0; w < 4; ++w)
+                                rk[u] += (t + w < nc4[u] && y[u][w] < x[u]) ? 1u : 0u;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const uint64_t b = __ballot(e < nc4[u] && rk[u] == bp.mpc - 1);
+                        if (b) {
+                            const int l = __builtin_ctzll(b);
+                            T4[u] = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(x[u] >> 32), l)
+                                     << 32) |
+                                    __builtin_amdgcn_readlane((uint32_t)x[u], l);
+                        }
+                    }
+                }
+                if (lane == 0) {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        if (nc4[u]) pool[sb4[u]] = T4[u];
+                }
+            }
+        }
+        wave_sync();
+        {
+            uint32_t rb[kWPPL], rc[kWPPL], rk[kWPPL];
+            uint64_t thr[kWPPL];
+#pragma unroll
+            for (int j = 0; j < kWPPL; ++j) {
+                const uint32_t q = (uint32_t)(pkv[j] >> pkb) & (kWCq - 1);
+                nc[j] = ((overm >> j) & 1u) ? pidm[q] >> 16 : 0u;
+                thr[j] = pool[((overm >> j) & 1u) ? sb[j] : 0u];
+            }
+            uint32_t shortm = 0;
+#pragma unroll
+            for (int j = 0; j < kWPPL; ++j) {
+                const bool over = (overm >> j) & 1u, cand = (candm >> j) & 1u;
+                const bool full = nc[j] >= bp.mpc;
+                if (over && full && !(cand && k64[j] <= thr[j])) keptm &= ~(1u << j);
+                if (over && !full && !cand) shortm |= 1u << j;
+            }
+            if (__ballot(shortm != 0)) {
+                uint32_t pos[kWPPL];
+#pragma unroll
+                for (int j = 0; j < kWPPL; ++j) {
+                    const uint32_t q = (uint32_t)(pkv[j] >> pkb) & (kWCq - 1);
+                    pos[j] = ((shortm >> j) & 1u) ? atomicAdd(&pidslot[q], 1u << 16) >> 16 : 0u;
+                }
+#pragma unroll
+                for (int j = 0; j < kWPPL; ++j)
+                    if ((shortm >> j) & 1u) pool[sb[j] + nc[j] + pos[j]] = k64[j];
+                wave_sync();
+                // C3: non-candidates of such pids rank among the appended ones
+#pragma unroll
+                for (int j = 0; j < kWPPL; ++j) {
+                    const uint32_t q = (uint32_t)(pkv[j] >> pkb) & (kWCq - 1);
+                    const bool sh = (shortm >> j) & 1u;
+                    rb[j] = sh ? sb[j] + nc[j] : 0u;
+                    rc[j] = sh ? pidslot[q] >> 16 : 0u;
+                }
+                rank_batch<kWPPL>(pool, rb, rc, k64, rk, jn);
+#pragma unroll
+                for (int j = 0; j < kWPPL; ++j)
+                    if (((shortm >> j) & 1u) && rk[j] >= bp.mpc - nc[j]) keptm &= ~(1u << j);
+            }
+        }
+        wave_sync();
+        mark(bp, 4, clk);
+        // ---- D: pair state; over-full kept pairs reserve one pool slot per
+        // record (the pool's mpc regions are dead now)
+        {
+            uint32_t c[kWPPL], b2[kWPPL];
+#pragma unroll
+            for (int j = 0; j < kWPPL; ++j) c[j] = pcnt[lane + 64u * j];
+#pragma unroll
+            for (int j = 0; j < kWPPL; ++j) {
+                const bool need = sample && ((keptm >> j) & 1u) && c[j] > bp.mcpp;
+                b2[j] = need ? atomicAdd(&bump[1], c[j]) : kKeptAll;
+            }
+#pragma unroll
+            for (int j = 0; j < kWPPL; ++j) {
+                if (lane + 64u * j < npair)
+                    pst[lane + 64u * j] = ((keptm >> j) & 1u) ? b2[j] : kDropped;
+                ecnt[j] = bp.mode == DPG_MODE_CROSS_AND_PER_PARTITION ? min(c[j], bp.mcpp) : c[j];
+            }
+        }
+        wave_sync();
+        mark(bp, 5, clk);
+        // ---- E: values of records of kept pairs are gathered; records of
+        // over-full kept pairs append their record key
+        uint64_t rkey[kWRPT];
+        double v[kWRPT];
+        uint32_t st[kWRPT];
+#pragma unroll
+        for (int k = 0; k < kWRPT; ++k) st[k] = pst[dn[k]];
+#pragma unroll
+        for (int k = 0; k < kWRPT; ++k) {
+            if (!((validm >> k) & 1u)) st[k] = kDropped;
+            if (st[k] < kKeptAll) st[k] &= 0xFFFFu;  // base (appends in the high bits)
+            v[k] = 0.0;
+            rkey[k] = 0;
+            if (need_v && st[k] != kDropped) v[k] = bp.value[RecOps<R>::idx(r[k], f)];
+        }
+        if (sample) {
+            uint32_t pv[kWRPT], pos[kWRPT];
+#pragma unroll
+            for (int k = 0; k < kWRPT; ++k) pv[k] = pidv[qs[k]];
+#pragma unroll
+            for (int k = 0; k < kWRPT; ++k) {
+                if (st[k] >= kKeptAll) continue;
+                const uint64_t key = RecOps<R>::key(r[k], f);
+                rkey[k] = rec_prio_h(pv[k], (uint32_t)(key & pkmask),
+                                     (uint64_t)(bp.rec_base + RecOps<R>::idx(r[k], f)));
+            }
+#pragma unroll
+            for (int k = 0; k < kWRPT; ++k)
+                pos[k] = st[k] < kKeptAll ? atomicAdd(&pst[dn[k]], 1u << 16) >> 16 : 0u;
+#pragma unroll
+            for (int k = 0; k < kWRPT; ++k)
+                if (st[k] < kKeptAll) pool[st[k] + pos[k]] = rkey[k];
+            wave_sync();
+        }
+        mark(bp, 6, clk);
+        // ---- F: a sampled record is kept iff fewer than mcpp keys of its
+        // pair are smaller; clipped accumulators of kept records
+        if (need_v) {
+            uint32_t keepm = 0;
+#pragma unroll
+            for (int k = 0; k < kWRPT; ++k) keepm |= st[k] == kKeptAll ? 1u << k : 0u;
+            if (sample) {
+                uint32_t rb[kWRPT], rc[kWRPT], rk[kWRPT];
+#pragma unroll
+                for (int k = 0; k < kWRPT; ++k) {
+                    const bool sm = st[k] < kKeptAll;
+                    rb[k] = sm ? st[k] : 0u;
+                    rc[k] = sm ? pcnt[dn[k]] : 0u;
+                }
+                rank_batch<kWRPT>(pool, rb, rc, rkey, rk, kn);
+#pragma unroll
+                for (int k = 0; k < kWRPT; ++k)
+                    if (st[k] < kKeptAll && rk[k] < bp.mcpp) keepm |= 1u << k;
+            }
+#pragma unroll
+            for (int k = 0; k < kWRPT; ++k) {
+                if (!((keepm >> k) & 1u)) continue;
+                const uint32_t p = dn[k];
+                if (part_clip) {
+                    atomicAdd(&acc_sum[p], v[k]);
+                } else {
+                    const double x = clampd(v[k], bp.lo, bp.hi);
+                    atomicAdd(&acc_sum[p], x);
+                    if (kVar) {
+                        const double y = x - bp.mid;
+                        atomicAdd(&acc_nsum[p], y);
+                        atomicAdd(&acc_nsq[p], y * y);
+                    }
+                }
+            }
+            wave_sync();
+        }
+        mark(bp, 7, clk);
+    } else {
+        // ---- PER_PRIVACY_ID: records of pids over L append their record key
+        // to the pid's region; a record is kept iff fewer than L records of
+        // its pid have a smaller key; pst counts kept records per pair
+        uint64_t rkey[kWRPT];
+        uint32_t sb[kWRPT], pv[kWRPT], pos[kWRPT], overm = 0;
+#pragma unroll
+        for (int k = 0; k < kWRPT; ++k) {
+            sb[k] = pidslot[qs[k]];
+            pv[k] = pidv[qs[k]];
+        }
+#pragma unroll
+        for (int k = 0; k < kWRPT; ++k) {
+            rkey[k] = 0;
+            if (!((validm >> k) & 1u) || sb[k] == kNil) continue;
+            overm |= 1u << k;
+            const uint64_t key = RecOps<R>::key(r[k], f);
+            rkey[k] = rec_prio_h(pv[k], (uint32_t)(key & pkmask),
+                                 (uint64_t)(bp.rec_base + RecOps<R>::idx(r[k], f)));
+        }
+#pragma unroll
+        for (int k = 0; k < kWRPT; ++k)
+            pos[k] = ((overm >> k) & 1u) ? atomicAdd(&pidm[qs[k]], 1u << 16) >> 16 : 0u;
+#pragma unroll
+        for (int k = 0; k < kWRPT; ++k)
+            if ((overm >> k) & 1u) pool[sb[k] + pos[k]] = rkey[k];
+        wave_sync();
+        mark(bp, 5, clk);
+        uint32_t rb[kWRPT], rc[kWRPT], rk[kWRPT];
+#pragma unroll
+        for (int k = 0; k < kWRPT; ++k) {
+            const bool o = (overm >> k) & 1u;
+            rb[k] = o ? sb[k] : 0u;
+            rc[k] = o ? pidm[qs[k]] & 0xFFFFu : 0u;
+        }
+        rank_batch<kWRPT>(pool, rb, rc, rkey, rk, kn);
+        double v[kWRPT];
+#pragma unroll
+        for (int k = 0; k < kWRPT; ++k) {
+            v[k] = 0.0;
+            if (((overm >> k) & 1u) && rk[k] >= bp.L) validm &= ~(1u << k);
+            if (need_v && ((validm >> k) & 1u)) v[k] = bp.value[RecOps<R>::idx(r[k], f)];
+        }
+#pragma unroll
+        for (int k = 0; k < kWRPT; ++k) {
+            if (!((validm >> k) & 1u)) continue;
+            const uint32_t p = dn[k];
+            atomicAdd(&pst[p], 1u);
+            if (need_v) {
+                if (part_clip) {
+                    atomicAdd(&acc_sum[p], v[k]);
+                } else {
+                    const double x = clampd(v[k], bp.lo, bp.hi);
+                    atomicAdd(&acc_sum[p], x);
+                    if (kVar) {
+                        const double y = x - bp.mid;
+                        atomicAdd(&acc_nsum[p], y);
+                        atomicAdd(&acc_nsq[p], y * y);
+                    }
+                }
+            }
+        }
+        wave_sync();
+        mark(bp, 7, clk);
+#pragma unroll
+        for (int j = 0; j < kWPPL; ++j) ecnt[j] = pst[lane + 64u * j];
+#pragma unroll
+        for (int j = 0; j < kWPPL; ++j)
+            if (lane + 64u * j < npair && ecnt[j] > 0) keptm |= 1u << j;
+    }
+    // ---- G: emit kept pairs; clear the key table
+    {
+        double a0[kWPPL], a1[kWPPL], a2[kWPPL];
+#pragma unroll
+        for (int j = 0; j < kWPPL; ++j) {
+            const uint32_t d = lane + 64u * j;
+            a0[j] = need_v ? acc_sum[d] : 0.0;
+            if constexpr (kVar) {
+                a1[j] = need_v ? acc_nsum[d] : 0.0;
+                a2[j] = need_v ? acc_nsq[d] : 0.0;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < kWPPL; ++j) {
+            const bool e = (keptm >> j) & 1u;
+            const uint64_t be = __ballot(e);
+            if (e) {
+                Item it;
+                it.pk = (uint32_t)(pkv[j] & (KeyT)pkmask);
+                it.cnt = ecnt[j];
+                it.sum = (need_v && part_clip) ? clampd(a0[j], bp.lo_pp, bp.hi_pp) : a0[j];
+                if constexpr (kVar) {
+                    it.nsum = a1[j];
+                    it.nsq = a2[j];
+                }
+                items[nitems + lanes_below(be)] = it;
+            }
+            nitems += (uint32_t)__popcll(be);
+        }
+        constexpr int kClr = (int)(sizeof(KeyT) * kWCk / (16 * 64));
+#pragma unroll
+        for (int i = 0; i < kClr; ++i)
+            reinterpret_cast<uint4 *>(keys)[lane + 64u * i] = make_uint4(~0u, ~0u, ~0u, ~0u);
+    }
+#pragma unroll
+    for (int j = 0; j < kWQPL; ++j)
+        if (lane + 64u * j < npid) pidm[qv[j]] = 0;
+    wave_sync();
+    mark(bp, 8, clk);
+    return nitems;
+}
+
+// Persistent single-wave workgroups walk the small-chunk list statically
+// (w, w + G, ...); workgroup g appends its items to items[wg_off[g], ...)
+// and leaves the count in wg_cnt[g].
+template <class KeyT, class Item, class R>
+__global__ __launch_bounds__(64) void k_bound_waves(const R *recs, const R *refined,
+                                                    const uint4 *chunks, const uint32_t *n_chunks,
+                                                    BoundParams bp, Item *items,
+                                                    const int64_t *wg_off, uint32_t *wg_cnt) {
+    using L = WaveLayout<KeyT, Item>;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    PhaseTimer clk;
+    timer_start(bp, clk);
+    const uint32_t nch = __builtin_amdgcn_readfirstlane(*n_chunks);
+    Item *my_items = items + wg_off[blockIdx.x];
+    const uint32_t lane = __lane_id();
+    {
+        uint32_t *pidm = reinterpret_cast<uint32_t *>(smem + L::PIDM);
+        KeyT *keys = reinterpret_cast<KeyT *>(smem + L::KEYS);
+        for (uint32_t i = lane; i < kWCq; i += 64) pidm[i] = 0;
+        for (uint32_t i = lane; i < kWCk; i += 64) keys[i] = empty_key<KeyT>();
+    }
+    wave_sync();
+    R r[kWRPT], rn[kWRPT];
+    const uint32_t G = gridDim.x;
+    uint32_t w = blockIdx.x;
+    uint32_t n = 0, d1 = 0, hb = 0, nitems = 0;
+    uint4 dn = make_uint4(0, 0, 0, 0);
+    if (w < nch) {
+        const uint4 d = chunks[w];
+        n = __builtin_amdgcn_readfirstlane(d.y & 0x7FFFFFFFu);
+        d1 = __builtin_amdgcn_readfirstlane(d.z);
+        hb = __builtin_amdgcn_readfirstlane(d.w);
+        const R *b = chunk_base(d, recs, refined);
+#pragma unroll
+        for (int k = 0; k < kWRPT; ++k) r[k] = b[min(lane + 64u * k, n - 1)];
+        if (w + G < nch) dn = chunks[w + G];
+    }
+    for (; w < nch; w += G) {
+        uint4 dnn = make_uint4(0, 0, 0, 0);
+        if (w + 2 * G < nch) dnn = chunks[w + 2 * G];
+        const uint4 du = make_uint4(__builtin_amdgcn_readfirstlane(dn.x),
+                                    __builtin_amdgcn_readfirstlane(dn.y),
+                                    __builtin_amdgcn_readfirstlane(dn.z),
+                                    __builtin_amdgcn_readfirstlane(dn.w));
+        const uint32_t nn = du.y & 0x7FFFFFFFu;
+        // the next chunk's records load while this one is processed
+        if (nn > 0) {
+            const R *nb = chunk_base(du, recs, refined);
+#pragma unroll
+            for (int k = 0; k < kWRPT; ++k) rn[k] = nb[min(lane + 64u * k, nn - 1)];
+        }
+        nitems = wave_chunk<KeyT, Item, R>(r, n, d1, hb, smem, bp, my_items, nitems, clk);
+#pragma unroll
+        for (int k = 0; k < kWRPT; ++k) r[k] = rn[k];
+        n = nn;
+        d1 = du.z;
+        hb = du.w;
+        dn = dnn;
+    }
+    if (lane == 0) wg_cnt[blockIdx.x] = nitems;
+    timer_flush(bp, clk);
+}
+
+}  // namespace dpg

@@ -18,7 +18,7 @@ def short(name: str) -> str:
     if not m:
         return name.split("(")[0][:60]
     base = m.group(1)
-    if m.group(3) and base in ("k_scatter", "k_hist", "k_reduce_items", "k_bound_chunks",
+    if m.group(3) and base in ("k_scatter", "k_hist", "k_reduce_items", "k_bound_chunks", "k_bound_waves",
                                "k_bound_big"):
         return f"{base}<{m.group(3)}>"
     return base
