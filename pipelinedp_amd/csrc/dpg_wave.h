@@ -98,6 +98,70 @@ __device__ __forceinline__ void rank_batch(const uint64_t *pool, const uint32_t 
     }
 }
 
+// Threshold search over key regions of the pool.  `mask` (uniform) selects
+// lanes whose (vb, vc) describe a region [vb, vb + vc) with vc >= K keys; for
+// every such region the K-th smallest key T is found and written over the
+// region's first entry, so that a key of the region is among the K smallest
+// iff it is <= T (keys are distinct).  Up to 4 regions at a time: lane e
+// holds entry e of each and counts the smaller keys of its region (the
+// region loads are lane-uniform, i.e. LDS broadcasts).
+__device__ __forceinline__ void region_thresholds(uint64_t *pool, uint64_t mask, uint32_t vb,
+                                                  uint32_t vc, uint32_t K) {
+    const uint32_t lane = __lane_id();
+    while (mask) {
+        uint32_t sb4[4], nc4[4], mxn = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            sb4[u] = 0;
+            nc4[u] = 0;
+            if (mask) {
+                const int l = __builtin_ctzll(mask);
+                mask &= mask - 1;
+                sb4[u] = __builtin_amdgcn_readlane(vb, l);
+                nc4[u] = __builtin_amdgcn_readlane(vc, l);
+            }
+            mxn = max(mxn, nc4[u]);
+        }
+        uint64_t T4[4] = {~0ull, ~0ull, ~0ull, ~0ull};
+        for (uint32_t l0 = 0; l0 < mxn; l0 += 64) {
+            const uint32_t e = l0 + lane;
+            uint64_t x[4];
+            uint32_t rk[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                x[u] = pool[sb4[u] + min(e, nc4[u] ? nc4[u] - 1 : 0u)];
+                rk[u] = 0;
+            }
+            for (uint32_t t = 0; t < mxn; t += 4) {
+                uint64_t y[4][4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+#pragma unroll
+                    for (int w = 0; w < 4; ++w)
+                        y[u][w] = pool[sb4[u] + min(t + w, nc4[u] ? nc4[u] - 1 : 0u)];
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) rk[u] += (t + w < nc4[u] && y[u][w] < x[u]) ? 1u : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint64_t b = __ballot(e < nc4[u] && rk[u] == K - 1);
+                if (b) {
+                    const int l = __builtin_ctzll(b);
+                    T4[u] = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(x[u] >> 32), l) << 32) |
+                            __builtin_amdgcn_readlane((uint32_t)x[u], l);
+                }
+            }
+        }
+        if (lane == 0) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (nc4[u]) pool[sb4[u]] = T4[u];
+        }
+    }
+}
+
 // Records past the chunk end hold a copy of its last record (loads are
 // unconditional); they aim their table CAS at lane-private dummy words and
 // take part in nothing that counts.  Every phase is written stage-wise over
@@ -308,10 +372,7 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
         // ---- C2: with >= mpc candidates, a candidate is kept iff fewer than
         // mpc candidates have a smaller key; with fewer (rare), every
         // candidate is kept and the non-candidates append after them (C3)
-        // Pid-major threshold search: for up to 4 pids at a time, lane e
-        // holds candidate e of each pid's region and counts the smaller keys
-        // (broadcast loads); the candidate of rank mpc - 1 is the pid's
-        // threshold, written over the region's first entry.
+        // threshold of every pid with >= mpc candidates (region_thresholds)
         {
             uint32_t psb[kWQPL], pnc[kWQPL];
 #pragma unroll
@@ -320,68 +381,11 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
                 pnc[j] = pidm[qv[j]] >> 16;
             }
 #pragma unroll
-            for (int j = 0; j < kWQPL; ++j) {
-                if (!(lane + 64u * j < npid && psb[j] != kNil && pnc[j] >= bp.mpc)) {
-                    psb[j] = 0;
-                    pnc[j] = 0;
-                }
-            }
-            for (uint32_t i0 = 0; i0 < npid; i0 += 4) {
-                uint32_t vs = psb[0], vn = pnc[0];
-#pragma unroll
-                for (int j = 1; j < kWQPL; ++j)
-                    if ((i0 >> 6) == (uint32_t)j) {
-                        vs = psb[j];
-                        vn = pnc[j];
-                    }
-                uint32_t sb4[4], nc4[4], mxn = 0;
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    sb4[u] = __builtin_amdgcn_readlane(vs, (i0 + u) & 63);
-                    nc4[u] = i0 + u < npid ? __builtin_amdgcn_readlane(vn, (i0 + u) & 63) : 0u;
-                    mxn = max(mxn, nc4[u]);
-                }
-                if (mxn == 0) continue;
-                uint64_t T4[4] = {~0ull, ~0ull, ~0ull, ~0ull};
-                for (uint32_t l0 = 0; l0 < mxn; l0 += 64) {
-                    const uint32_t e = l0 + lane;
-                    uint64_t x[4];
-                    uint32_t rk[4];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        x[u] = pool[sb4[u] + min(e, nc4[u] ? nc4[u] - 1 : 0u)];
-                        rk[u] = 0;
-                    }
-                    for (uint32_t t = 0; t < mxn; t += 4) {
-                        uint64_t y[4][4];
-#pragma unroll
-                        for (int u = 0; u < 4; ++u)
-#pragma unroll
-                            for (int w = 0; w < 4; ++w)
-                                y[u][w] = pool[sb4[u] + min(t + w, nc4[u] ? nc4[u] - 1 : 0u)];
-#pragma unroll
-                        for (int u = 0; u < 4; ++u)
-#pragma unroll
-                            for (int w = 0; w < 4; ++w)
-                                rk[u] += (t + w < nc4[u] && y[u][w] < x[u]) ? 1u : 0u;
-                    }
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const uint64_t b = __ballot(e < nc4[u] && rk[u] == bp.mpc - 1);
-                        if (b) {
-                            const int l = __builtin_ctzll(b);
-                            T4[u] = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(x[u] >> 32), l)
-                                     << 32) |
-                                    __builtin_amdgcn_readlane((uint32_t)x[u], l);
-                        }
-                    }
-                }
-                if (lane == 0) {
-#pragma unroll
-                    for (int u = 0; u < 4; ++u)
-                        if (nc4[u]) pool[sb4[u]] = T4[u];
-                }
-            }
+            for (int j = 0; j < kWQPL; ++j)
+                region_thresholds(pool,
+                                  __ballot(lane + 64u * j < npid && psb[j] != kNil &&
+                                           pnc[j] >= bp.mpc),
+                                  psb[j], pnc[j], bp.mpc);
         }
         wave_sync();
         {
@@ -430,8 +434,8 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
         mark(bp, 4, clk);
         // ---- D: pair state; over-full kept pairs reserve one pool slot per
         // record (the pool's mpc regions are dead now)
+        uint32_t c[kWPPL], b2[kWPPL];
         {
-            uint32_t c[kWPPL], b2[kWPPL];
 #pragma unroll
             for (int j = 0; j < kWPPL; ++j) c[j] = pcnt[lane + 64u * j];
 #pragma unroll
@@ -490,17 +494,18 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
 #pragma unroll
             for (int k = 0; k < kWRPT; ++k) keepm |= st[k] == kKeptAll ? 1u << k : 0u;
             if (sample) {
-                uint32_t rb[kWRPT], rc[kWRPT], rk[kWRPT];
+                // threshold of every over-full kept pair; a sampled record is
+                // kept iff its key is <= the threshold
 #pragma unroll
-                for (int k = 0; k < kWRPT; ++k) {
-                    const bool sm = st[k] < kKeptAll;
-                    rb[k] = sm ? st[k] : 0u;
-                    rc[k] = sm ? pcnt[dn[k]] : 0u;
-                }
-                rank_batch<kWRPT>(pool, rb, rc, rkey, rk, kn);
+                for (int j = 0; j < kWPPL; ++j)
+                    region_thresholds(pool, __ballot(b2[j] < kKeptAll), b2[j], c[j], bp.mcpp);
+                wave_sync();
+                uint64_t thr[kWRPT];
+#pragma unroll
+                for (int k = 0; k < kWRPT; ++k) thr[k] = pool[st[k] < kKeptAll ? st[k] : 0u];
 #pragma unroll
                 for (int k = 0; k < kWRPT; ++k)
-                    if (st[k] < kKeptAll && rk[k] < bp.mcpp) keepm |= 1u << k;
+                    if (st[k] < kKeptAll && rkey[k] <= thr[k]) keepm |= 1u << k;
             }
 #pragma unroll
             for (int k = 0; k < kWRPT; ++k) {
@@ -549,19 +554,27 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
             if ((overm >> k) & 1u) pool[sb[k] + pos[k]] = rkey[k];
         wave_sync();
         mark(bp, 5, clk);
-        uint32_t rb[kWRPT], rc[kWRPT], rk[kWRPT];
+        {
+            uint32_t psb[kWQPL], pnc[kWQPL];
 #pragma unroll
-        for (int k = 0; k < kWRPT; ++k) {
-            const bool o = (overm >> k) & 1u;
-            rb[k] = o ? sb[k] : 0u;
-            rc[k] = o ? pidm[qs[k]] & 0xFFFFu : 0u;
+            for (int j = 0; j < kWQPL; ++j) {
+                psb[j] = pidslot[qv[j]];
+                pnc[j] = pidm[qv[j]] & 0xFFFFu;
+            }
+#pragma unroll
+            for (int j = 0; j < kWQPL; ++j)
+                region_thresholds(pool, __ballot(lane + 64u * j < npid && psb[j] != kNil), psb[j],
+                                  pnc[j], bp.L);
         }
-        rank_batch<kWRPT>(pool, rb, rc, rkey, rk, kn);
+        wave_sync();
+        uint64_t thr[kWRPT];
+#pragma unroll
+        for (int k = 0; k < kWRPT; ++k) thr[k] = pool[((overm >> k) & 1u) ? sb[k] : 0u];
         double v[kWRPT];
 #pragma unroll
         for (int k = 0; k < kWRPT; ++k) {
             v[k] = 0.0;
-            if (((overm >> k) & 1u) && rk[k] >= bp.L) validm &= ~(1u << k);
+            if (((overm >> k) & 1u) && rkey[k] > thr[k]) validm &= ~(1u << k);
             if (need_v && ((validm >> k) & 1u)) v[k] = bp.value[RecOps<R>::idx(r[k], f)];
         }
 #pragma unroll
