@@ -166,13 +166,14 @@ void dpg_ctx_destroy(dpg_ctx *ctx);
 int dpg_last_error(dpg_ctx *ctx, char *buf, size_t len);
 int dpg_set_seed(dpg_ctx *ctx, uint64_t seed);
 
-/* Tuning / testing hook: average records per privacy-id bucket the
- * partition levels aim for (default: half the chunk capacity; smaller values
- * force more levels on small inputs) and the chunk capacity, i.e. the most
- * records bounded together in LDS (default and maximum 2048 for COUNT/SUM,
- * 1536 with MEAN/VARIANCE).  Buckets over the capacity are split by further
- * privacy-id hash bits; a bucket still over it takes the global-memory path.
- * <= 0 keeps the current value. */
+/* Tuning / testing hook: average records per fine privacy-id bucket the
+ * partition levels aim for (default 256; smaller values force more levels on
+ * small inputs) and the chunk capacity, i.e. the most records bounded
+ * together in LDS (default and maximum 1024; chunks of <= min(cap, 512)
+ * records run one wave each, larger ones one 256-thread workgroup).  Buckets
+ * over the capacity are split by further privacy-id hash bits; a bucket
+ * still over it takes the global-memory path.  <= 0 keeps the current
+ * value. */
 int dpg_set_tuning(dpg_ctx *ctx, int32_t bucket_target, int32_t bucket_cap);
 
 /* Contribution bounding + per-(pid,pk) accumulators + merge per partition.

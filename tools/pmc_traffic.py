@@ -16,13 +16,13 @@ import sys
 
 
 def short(name: str) -> str:
-    m = re.search(r"dpg::(k_\w+)(<([^,>]*))?", name)
+    # same naming as bench.py's dominant-kernel map: k_scatter<SrcSoAKey>, ...
+    m = re.search(r"dpg::(k_\w+)(<(?:dpg::)?(\w+))?", name)
     if not m:
         return name.split("(")[0][:60]
     base = m.group(1)
     if m.group(3) and base in ("k_scatter", "k_hist", "k_reduce_items"):
-        arg = m.group(3).replace("dpg::", "")
-        return f"{base}<{arg}>"
+        return f"{base}<{m.group(3)}>"
     return base
 
 
