@@ -195,7 +195,7 @@ int run_level(dpg_ctx *ctx, hipStream_t s, const Src &src, uint32_t S, const int
               uint32_t *ntiles_dev, const int64_t *out_start = nullptr) {
     int st = DPG_OK;
     if (F > (uint32_t)FMAX) return fail(ctx, DPG_ERR_HIP, "internal: digit fan-out too large");
-    const int64_t sub = (int64_t)kPartThreads * IPT;
+    const int64_t sub = (int64_t)kScatThreads * IPT;
     const int64_t tile = std::max<int64_t>(sub, ((n_upper / 3072 + sub - 1) / sub) * sub);
     const uint32_t max_tiles = (uint32_t)(n_upper / tile + S + 1);
     std::string t(tag);
@@ -218,11 +218,12 @@ int run_level(dpg_ctx *ctx, hipStream_t s, const Src &src, uint32_t S, const int
     LAUNCH_CHECK();
     constexpr size_t lds = scatter_lds<Src, Rec, IPT, FMAX>();
     static_assert(lds <= 160 * 1024, "scatter LDS");
-    (void)hipFuncSetAttribute((const void *)k_scatter<Src, Rec, IPT, FMAX>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    // few digits: wave-aggregated ranking; otherwise one LDS atomic per record
+    auto kern = bits > 4 ? k_scatter<Src, Rec, IPT, FMAX, false> : k_scatter<Src, Rec, IPT, FMAX, true>;
+    (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
     stage(ctx, s, (t + ":scatter").c_str());
-    k_scatter<Src, Rec, IPT, FMAX><<<max_tiles, kPartThreads, lds, s>>>(src, tiles, ntiles_dev, F,
-                                                                         bits, hist, base, out);
+    kern<<<max_tiles, kScatThreads, lds, s>>>(src, tiles, ntiles_dev, F, bits, hist, base, out);
     LAUNCH_CHECK();
     *base_out = base;
     *tot_out = tot;

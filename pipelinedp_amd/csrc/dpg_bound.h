@@ -55,11 +55,11 @@ __device__ __forceinline__ uint64_t pid_of(const BoundParams &bp, uint32_t d1, u
 }
 
 // Debug hooks at phase boundaries: watchdog progress, and (DPG_PHASE_TIMING)
-// the shader cycles thread 0 spent since the previous mark, added to the
-// register accumulator pt[phase]; the kernel flushes pt once at exit.
+// the shader cycles thread 0 spent since the previous mark, added straight to
+// the global counter phase_cyc[phase] (only the last timestamp lives in
+// registers, so the hook costs no scalar registers when timing is off).
 struct PhaseTimer {
     uint64_t last;
-    uint64_t pt[10];
 };
 __device__ __forceinline__ void mark(const BoundParams &bp, uint32_t phase, PhaseTimer &tm) {
     if (bp.progress && threadIdx.x == 0)
@@ -67,18 +67,14 @@ __device__ __forceinline__ void mark(const BoundParams &bp, uint32_t phase, Phas
                            __HIP_MEMORY_SCOPE_SYSTEM);
     if (bp.phase_cyc) {
         const uint64_t now = __builtin_amdgcn_s_memtime();
-        tm.pt[phase] += now - tm.last;
+        if (threadIdx.x == 0) atomicAdd(&bp.phase_cyc[phase], (unsigned long long)(now - tm.last));
         tm.last = now;
     }
 }
 __device__ __forceinline__ void timer_start(const BoundParams &bp, PhaseTimer &tm) {
     tm.last = bp.phase_cyc ? __builtin_amdgcn_s_memtime() : 0;
-    for (int k = 0; k < 10; ++k) tm.pt[k] = 0;
 }
-__device__ __forceinline__ void timer_flush(const BoundParams &bp, const PhaseTimer &tm) {
-    if (bp.phase_cyc && threadIdx.x == 0)
-        for (int k = 0; k < 10; ++k) atomicAdd(&bp.phase_cyc[k], (unsigned long long)tm.pt[k]);
-}
+__device__ __forceinline__ void timer_flush(const BoundParams &, const PhaseTimer &) {}
 
 __host__ __device__ __forceinline__ uint32_t next_pow2(uint32_t x) {
     uint32_t p = 64;

@@ -20,6 +20,9 @@
 namespace dpg {
 
 constexpr int kPartThreads = 1024;  // 16 waves
+// scatter workgroups (512 threads with twice the records per thread measured
+// slower on the level-1 scatter)
+constexpr int kScatThreads = 1024;
 
 __host__ __device__ constexpr size_t a16(size_t x) { return (x + 15) & ~(size_t)15; }
 
@@ -267,6 +270,51 @@ __device__ __forceinline__ uint32_t block_scan_digits(const uint32_t *cnt, uint3
     return total;
 }
 
+// Block-wide exclusive scan of one value per thread (T threads, T / 64
+// waves <= 16).
+template <int T>
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t *sh16, uint32_t &total) {
+    constexpr int NW = T / 64;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t wt;
+    uint32_t e = wave_excl_scan(x, wt);
+    if (lane == 63) sh16[w] = wt;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+        uint32_t y = sh16[k];
+        if (k < w) pre += y;
+        tot += y;
+    }
+    __syncthreads();
+    total = tot;
+    return e + pre;
+}
+
+// Exclusive scan of cnt[0, F) (F <= DPT * T) into dstart by T threads (DPT
+// consecutive digits per thread); returns the total.  Ends with a barrier.
+template <int T, int DPT>
+__device__ __forceinline__ uint32_t block_scan_digits_t(const uint32_t *cnt, uint32_t *dstart,
+                                                        uint32_t F, uint32_t *sh16) {
+    const uint32_t d0 = DPT * threadIdx.x;
+    uint32_t c[DPT], s = 0;
+#pragma unroll
+    for (int u = 0; u < DPT; ++u) {
+        c[u] = d0 + u < F ? cnt[d0 + u] : 0u;
+        s += c[u];
+    }
+    uint32_t total;
+    uint32_t e = block_excl_scan<T>(s, sh16, total);
+#pragma unroll
+    for (int u = 0; u < DPT; ++u) {
+        if (d0 + u < F) dstart[d0 + u] = e;
+        e += c[u];
+    }
+    __syncthreads();
+    return total;
+}
+
 // grid S: base[s][d] = seg_start[s] + exclusive_prefix_d(tot[s][.])  (F <= 2048)
 __global__ __launch_bounds__(1024) void k_digit_base(const int64_t *seg_start, uint32_t F,
                                                      const uint32_t *tot, int64_t *base) {
@@ -330,17 +378,20 @@ __device__ __forceinline__ T from_words(const Words<T> &x) {
 // LDS bytes of one k_scatter instantiation.
 template <class Src, class Rec, int IPT, int FMAX>
 constexpr size_t scatter_lds() {
-    return (size_t)sizeof(Rec) * kPartThreads * IPT +
-           (Src::kDigitFromRec ? 0 : a16((size_t)2 * kPartThreads * IPT)) + (size_t)FMAX * 12 +
+    return (size_t)sizeof(Rec) * kScatThreads * IPT +
+           (Src::kDigitFromRec ? 0 : a16((size_t)2 * kScatThreads * IPT)) + (size_t)FMAX * 12 +
            64;
 }
 
-template <class Src, class Rec, int IPT, int FMAX>
-__global__ __launch_bounds__(kPartThreads) void k_scatter(Src src_in, const TileDesc *tiles,
+// kAgg: wave-aggregated ranking (few digits) instead of one LDS atomic per
+// record; a template parameter so that each kernel holds one ranking path
+// (both paths in one kernel cost the hot one its registers)
+template <class Src, class Rec, int IPT, int FMAX, bool kAgg>
+__global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const TileDesc *tiles,
                                                           const uint32_t *ntiles, uint32_t F,
                                                           uint32_t bits, const uint32_t *off,
                                                           const int64_t *base, Rec *out) {
-    constexpr int SUB = kPartThreads * IPT;
+    constexpr int SUB = kScatThreads * IPT;
     constexpr bool kSD = !Src::kDigitFromRec;
     using W = Words<Rec>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -357,7 +408,7 @@ __global__ __launch_bounds__(kPartThreads) void k_scatter(Src src_in, const Tile
     const TileDesc td = tiles[t];
     const int tid = threadIdx.x;
     Src src = src_in;  // per-thread copy (sources may cache lookup state)
-    for (uint32_t d = tid; d < F; d += kPartThreads) {
+    for (uint32_t d = tid; d < F; d += kScatThreads) {
         cur[d] = (uint32_t)(base[(size_t)td.seg * F + d] + off[(size_t)t * F + d]);
         cnt[d] = 0;
     }
@@ -372,19 +423,19 @@ __global__ __launch_bounds__(kPartThreads) void k_scatter(Src src_in, const Tile
         const uint32_t lim = (uint32_t)min<int64_t>(SUB, td.end - td.begin);
 #pragma unroll
         for (int j = 0; j < IPT; ++j)
-            raw[j] = src.fetch(td.begin + min((uint32_t)(j * kPartThreads + tid), lim - 1));
+            raw[j] = src.fetch(td.begin + min((uint32_t)(j * kScatThreads + tid), lim - 1));
     }
     __syncthreads();
     for (int64_t sb = td.begin; sb < td.end; sb += SUB) {
         const uint32_t lim = (uint32_t)min<int64_t>(SUB, td.end - sb);  // uniform
         Rec rec[IPT];
         uint32_t dr[IPT];  // digit | rank << 12, or ~0 for a dropped record
-        if (bits > 4) {
+        if constexpr (!kAgg) {
             // wide fan-out: one LDS atomic per record ranks it (order inside
             // a digit is free); all IPT atomics are in flight together
 #pragma unroll
             for (int j = 0; j < IPT; ++j) {
-                const uint32_t o = j * kPartThreads + tid;
+                const uint32_t o = j * kScatThreads + tid;
                 uint32_t d = 0;
                 const bool ok = o < lim && src.decode(raw[j], sb + o, rec[j], d);
                 dr[j] = ok ? d : ~0u;
@@ -397,7 +448,7 @@ __global__ __launch_bounds__(kPartThreads) void k_scatter(Src src_in, const Tile
             // serialisation
 #pragma unroll
             for (int j = 0; j < IPT; ++j) {
-                const uint32_t o = j * kPartThreads + tid;
+                const uint32_t o = j * kScatThreads + tid;
                 uint32_t d = 0;
                 const bool ok = o < lim && src.decode(raw[j], sb + o, rec[j], d);
                 const uint32_t rk = wave_agg_rank(cnt, ok ? d : 0u, ok, bits);
@@ -405,7 +456,8 @@ __global__ __launch_bounds__(kPartThreads) void k_scatter(Src src_in, const Tile
             }
         }
         __syncthreads();
-        const uint32_t total = block_scan_digits(cnt, dstart, F, sh16);
+        const uint32_t total =
+            block_scan_digits_t<kScatThreads, FMAX / kScatThreads>(cnt, dstart, F, sh16);
 #pragma unroll
         for (int j = 0; j < IPT; ++j)
             if (dr[j] != ~0u) {
@@ -420,30 +472,30 @@ __global__ __launch_bounds__(kPartThreads) void k_scatter(Src src_in, const Tile
         if (nlim > 0) {
 #pragma unroll
             for (int j = 0; j < IPT; ++j)
-                raw[j] = src.fetch(nb + min((uint32_t)(j * kPartThreads + tid), nlim - 1));
+                raw[j] = src.fetch(nb + min((uint32_t)(j * kScatThreads + tid), nlim - 1));
         }
         // write-out in batches of WB staged records per thread: the LDS reads
         // of a batch are in flight together, stores are predicated
         constexpr int WB = IPT < 8 ? IPT : 8;
-        for (uint32_t k0 = 0; k0 < total; k0 += WB * kPartThreads) {
+        for (uint32_t k0 = 0; k0 < total; k0 += WB * kScatThreads) {
             W x[WB];
             uint32_t dd[WB];
 #pragma unroll
             for (int u = 0; u < WB; ++u) {
-                const uint32_t k = min(k0 + u * kPartThreads + tid, total - 1);
+                const uint32_t k = min(k0 + u * kScatThreads + tid, total - 1);
                 x[u] = stage[k];
                 if constexpr (kSD) dd[u] = sdig[k];
                 else dd[u] = src.digit(from_words<Rec>(x[u]));
             }
 #pragma unroll
             for (int u = 0; u < WB; ++u) {
-                const uint32_t k = k0 + u * kPartThreads + tid;
+                const uint32_t k = k0 + u * kScatThreads + tid;
                 const uint32_t dst = cur[dd[u]] - dstart[dd[u]] + k;
                 if (k < total) *reinterpret_cast<W *>(&out[dst]) = x[u];
             }
         }
         __syncthreads();
-        for (uint32_t d = tid; d < F; d += kPartThreads) {
+        for (uint32_t d = tid; d < F; d += kScatThreads) {
             cur[d] += cnt[d];
             cnt[d] = 0;
         }

@@ -33,6 +33,17 @@
 namespace dpg {
 
 
+// Hide a uniform value from the compiler's uniformity analysis so that it
+// lives in a VGPR: the wave kernel runs short of scalar registers (spills
+// cost v_writelane / v_readlane issue slots), while vector registers have
+// headroom.  For parameters used in few places only.
+template <class T>
+__device__ __forceinline__ T vreg(T x) {
+    static_assert(sizeof(T) == 4 || sizeof(T) == 8, "vreg");
+    asm volatile("" : "=v"(x) : "0"(x));
+    return x;
+}
+
 template <class KeyT, class Item>
 struct WaveLayout {
     static constexpr bool var = ItemTraits<Item>::var;
@@ -658,6 +669,18 @@ __global__ __launch_bounds__(64) void k_bound_waves(const R *recs, const R *refi
     extern __shared__ __attribute__((aligned(16))) char smem[];
     PhaseTimer clk;
     timer_start(bp, clk);
+    // parameters used in one phase each: vector registers (see vreg)
+    bp.lo = vreg(bp.lo);
+    bp.hi = vreg(bp.hi);
+    bp.lo_pp = vreg(bp.lo_pp);
+    bp.hi_pp = vreg(bp.hi_pp);
+    bp.mid = vreg(bp.mid);
+    bp.seed = vreg(bp.seed);
+    bp.pid_min = vreg(bp.pid_min);
+    bp.rec_base = vreg(bp.rec_base);
+    bp.hash.mask = vreg(bp.hash.mask);
+    bp.hash.i1 = vreg(bp.hash.i1);
+    bp.hash.i2 = vreg(bp.hash.i2);
     const uint32_t nch = __builtin_amdgcn_readfirstlane(*n_chunks);
     Item *my_items = items + wg_off[blockIdx.x];
     const uint32_t lane = __lane_id();
