@@ -368,9 +368,12 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     // writes its items to items[wg_off[g], ...)
     // resident single-wave workgroups per CU: the LDS share or the register
     // file, whichever binds (a static schedule must not oversubscribe)
+    // one kernel per bounding family (PER_PRIVACY_ID or cross-partition), so
+    // that the hot one holds one path only
+    const bool per_pid = bp.mode == DPG_MODE_PER_PRIVACY_ID;
+    auto wave_kern = per_pid ? k_bound_waves<KeyT, Item, R, true> : k_bound_waves<KeyT, Item, R, false>;
     int wpc = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&wpc, k_bound_waves<KeyT, Item, R>, 64,
-                                                     WL::TOTAL) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&wpc, wave_kern, 64, WL::TOTAL) != hipSuccess ||
         wpc <= 0)
         wpc = 1;
     const uint32_t Gw = (uint32_t)(ctx->n_cu * std::min(wpc, WL::PER_CU));
@@ -402,10 +405,10 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
         HIP_TRY(hipMemsetAsync(pc, 0, 32 * 8, s));
         bpl.phase_cyc = pc;
     }
-    (void)hipFuncSetAttribute((const void *)k_bound_waves<KeyT, Item, R>,
+    (void)hipFuncSetAttribute((const void *)wave_kern,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)WL::TOTAL);
     stage(ctx, s, "bound");
-    k_bound_waves<KeyT, Item, R><<<Gw, 64, WL::TOTAL, s>>>(recs, refined, chunk_list,
+    wave_kern<<<Gw, 64, WL::TOTAL, s>>>(recs, refined, chunk_list,
                                                           &ctl->n_chunks, bpl, items, wg_off,
                                                           wg_cnt);
     LAUNCH_CHECK();

@@ -179,7 +179,7 @@ __device__ __forceinline__ void region_thresholds(uint64_t *pool, uint64_t mask,
 // the lane's kWRPT records / kWPPL pairs (all loads of a stage issued before
 // any use), so one wave keeps many LDS round trips in flight.  Pairs get
 // dense ids 0..npair-1 when they are created; every per-pair array is dense.
-template <class KeyT, class Item, class R>
+template <class KeyT, class Item, class R, bool kPerPid>
 __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, uint32_t d1,
                                                uint32_t hbase, char *smem, const BoundParams &bp,
                                                Item *items, uint32_t nitems, PhaseTimer &clk) {
@@ -203,7 +203,7 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
     const Fmt f = bp.fmt;
     const uint32_t pkb = f.pkbits;
     const uint64_t pkmask = (1ull << pkb) - 1ull;
-    const bool per_pid = bp.mode == DPG_MODE_PER_PRIVACY_ID;
+    constexpr bool per_pid = kPerPid;  // bp.mode == DPG_MODE_PER_PRIVACY_ID
     const bool need_v = bp.need_values != 0;
     const bool sample = bp.mode == DPG_MODE_CROSS_AND_PER_PARTITION && need_v;
     const bool part_clip = bp.sum_mode == DPG_SUM_CLIP_PARTITION;
@@ -341,7 +341,7 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
     uint32_t keptm = 0, ecnt[kWPPL];
 #pragma unroll
     for (int j = 0; j < kWPPL; ++j) pkv[j] = pkey_d[lane + 64u * j];
-    if (!per_pid) {
+    if constexpr (!per_pid) {
         // ---- C1: candidates (priority below the pid's threshold) append
         // their pair key to the pid's region
         uint32_t sb[kWPPL], nc[kWPPL];
@@ -660,7 +660,7 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
 // Persistent single-wave workgroups walk the small-chunk list statically
 // (w, w + G, ...); workgroup g appends its items to items[wg_off[g], ...)
 // and leaves the count in wg_cnt[g].
-template <class KeyT, class Item, class R>
+template <class KeyT, class Item, class R, bool kPerPid>
 __global__ __launch_bounds__(64) void k_bound_waves(const R *recs, const R *refined,
                                                     const uint4 *chunks, const uint32_t *n_chunks,
                                                     BoundParams bp, Item *items,
@@ -720,7 +720,7 @@ __global__ __launch_bounds__(64) void k_bound_waves(const R *recs, const R *refi
 #pragma unroll
             for (int k = 0; k < kWRPT; ++k) rn[k] = nb[min(lane + 64u * k, nn - 1)];
         }
-        nitems = wave_chunk<KeyT, Item, R>(r, n, d1, hb, smem, bp, my_items, nitems, clk);
+        nitems = wave_chunk<KeyT, Item, R, kPerPid>(r, n, d1, hb, smem, bp, my_items, nitems, clk);
 #pragma unroll
         for (int k = 0; k < kWRPT; ++k) r[k] = rn[k];
         n = nn;
