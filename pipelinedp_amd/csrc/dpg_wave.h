@@ -113,64 +113,79 @@ __device__ __forceinline__ void rank_batch(const uint64_t *pool, const uint32_t 
 // lanes whose (vb, vc) describe a region [vb, vb + vc) with vc >= K keys; for
 // every such region the K-th smallest key T is found and written over the
 // region's first entry, so that a key of the region is among the K smallest
-// iff it is <= T (keys are distinct).  Up to 4 regions at a time: lane e
-// holds entry e of each and counts the smaller keys of its region (the
-// region loads are lane-uniform, i.e. LDS broadcasts).
+// iff it is <= T (keys are distinct).
+//
+// Regions of <= 64 keys are packed side by side into the wave's lanes (lane
+// = one entry of one region); each lane counts the smaller keys of its own
+// region, 4 per load batch, and the entry of rank K - 1 writes the
+// threshold itself.  Larger regions (rare) take region_thresholds_wide.
+__device__ __forceinline__ void region_thresholds_wide(uint64_t *pool, uint64_t mask, uint32_t vb,
+                                                       uint32_t vc, uint32_t K) {
+    const uint32_t lane = __lane_id();
+    while (mask) {
+        const int l = __builtin_ctzll(mask);
+        mask &= mask - 1;
+        const uint32_t sb = __builtin_amdgcn_readlane(vb, l);
+        const uint32_t nc = __builtin_amdgcn_readlane(vc, l);
+        uint64_t T = ~0ull;
+        for (uint32_t l0 = 0; l0 < nc; l0 += 64) {
+            const uint32_t e = l0 + lane;
+            const uint64_t x = pool[sb + min(e, nc - 1)];
+            uint32_t rk = 0;
+            for (uint32_t t = 0; t < nc; t += 4) {
+                uint64_t y[4];
+#pragma unroll
+                for (int w = 0; w < 4; ++w) y[w] = pool[sb + min(t + w, nc - 1)];
+#pragma unroll
+                for (int w = 0; w < 4; ++w) rk += (t + w < nc && y[w] < x) ? 1u : 0u;
+            }
+            const uint64_t b = __ballot(e < nc && rk == K - 1);
+            if (b) {
+                const int m = __builtin_ctzll(b);
+                T = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(x >> 32), m) << 32) |
+                    __builtin_amdgcn_readlane((uint32_t)x, m);
+            }
+        }
+        if (lane == 0) pool[sb] = T;
+    }
+}
+
 __device__ __forceinline__ void region_thresholds(uint64_t *pool, uint64_t mask, uint32_t vb,
                                                   uint32_t vc, uint32_t K) {
     const uint32_t lane = __lane_id();
+    const uint64_t big = mask & __ballot(vc > 64);
+    mask &= ~big;
     while (mask) {
-        uint32_t sb4[4], nc4[4], mxn = 0;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            sb4[u] = 0;
-            nc4[u] = 0;
-            if (mask) {
-                const int l = __builtin_ctzll(mask);
-                mask &= mask - 1;
-                sb4[u] = __builtin_amdgcn_readlane(vb, l);
-                nc4[u] = __builtin_amdgcn_readlane(vc, l);
-            }
-            mxn = max(mxn, nc4[u]);
+        // pack regions into lanes [off, off + c)
+        uint32_t my_b = 0, my_c = 0, my_off = 0, used = 0, maxc = 0;
+        for (uint64_t m = mask; m; m &= m - 1) {
+            const int l = __builtin_ctzll(m);
+            const uint32_t c = __builtin_amdgcn_readlane(vc, l);
+            if (used + c > 64) break;
+            const uint32_t b = __builtin_amdgcn_readlane(vb, l);
+            const bool inr = lane >= used && lane < used + c;
+            my_b = inr ? b : my_b;
+            my_c = inr ? c : my_c;
+            my_off = inr ? used : my_off;
+            used += c;
+            maxc = max(maxc, c);
+            mask &= ~(1ull << l);
         }
-        uint64_t T4[4] = {~0ull, ~0ull, ~0ull, ~0ull};
-        for (uint32_t l0 = 0; l0 < mxn; l0 += 64) {
-            const uint32_t e = l0 + lane;
-            uint64_t x[4];
-            uint32_t rk[4];
+        const bool act = lane < used;
+        const uint32_t last = my_c ? my_c - 1 : 0u;
+        const uint64_t x = pool[my_b + min(lane - my_off, last)];
+        uint32_t rk = 0;
+        for (uint32_t t = 0; t < maxc; t += 4) {
+            uint64_t y[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                x[u] = pool[sb4[u] + min(e, nc4[u] ? nc4[u] - 1 : 0u)];
-                rk[u] = 0;
-            }
-            for (uint32_t t = 0; t < mxn; t += 4) {
-                uint64_t y[4][4];
+            for (int w = 0; w < 4; ++w) y[w] = pool[my_b + min(t + w, last)];
 #pragma unroll
-                for (int u = 0; u < 4; ++u)
-#pragma unroll
-                    for (int w = 0; w < 4; ++w)
-                        y[u][w] = pool[sb4[u] + min(t + w, nc4[u] ? nc4[u] - 1 : 0u)];
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-#pragma unroll
-                    for (int w = 0; w < 4; ++w) rk[u] += (t + w < nc4[u] && y[u][w] < x[u]) ? 1u : 0u;
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const uint64_t b = __ballot(e < nc4[u] && rk[u] == K - 1);
-                if (b) {
-                    const int l = __builtin_ctzll(b);
-                    T4[u] = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(x[u] >> 32), l) << 32) |
-                            __builtin_amdgcn_readlane((uint32_t)x[u], l);
-                }
-            }
+            for (int w = 0; w < 4; ++w) rk += (t + w < my_c && y[w] < x) ? 1u : 0u;
         }
-        if (lane == 0) {
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if (nc4[u]) pool[sb4[u]] = T4[u];
-        }
+        // every lane of the pass has read its region: the threshold may land
+        if (act && rk == K - 1) pool[my_b] = x;
     }
+    if (big) region_thresholds_wide(pool, big, vb, vc, K);
 }
 
 // Records past the chunk end hold a copy of its last record (loads are
