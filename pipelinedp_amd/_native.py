@@ -87,12 +87,16 @@ def load():
     with _lock:
         if _lib is not None:
             return _lib
-        if not os.path.exists(_LIB_PATH):
+        path = _LIB_PATH
+        if os.environ.get("DPG_PHASE_TIMING"):
+            # debug build with per-phase cycle counters (tools/gpu_phase.sh)
+            path = _LIB_PATH.replace("libdpg.so", "libdpg_timing.so")
+        if not os.path.exists(path):
             raise NativeError(
-                f"{_LIB_PATH} is missing: build it with "
+                f"{path} is missing: build it with "
                 f"`python -c 'import __graft_entry__ as g; g.build()'`. "
                 f"There is no CPU fallback for the MI355X hot path.")
-        lib = ctypes.CDLL(_LIB_PATH)
+        lib = ctypes.CDLL(path)
         vp, i64, i32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32
         lib.dpg_ctx_create.argtypes = [ctypes.c_int, ctypes.c_uint64]
         lib.dpg_ctx_create.restype = vp

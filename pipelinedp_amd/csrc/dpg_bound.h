@@ -54,27 +54,52 @@ __device__ __forceinline__ uint64_t pid_of(const BoundParams &bp, uint32_t d1, u
     return (uint64_t)(bp.pid_min + (int64_t)hk_inv(h, bp.hash));
 }
 
-// Debug hooks at phase boundaries: watchdog progress, and (DPG_PHASE_TIMING)
-// the shader cycles thread 0 spent since the previous mark, added straight to
-// the global counter phase_cyc[phase] (only the last timestamp lives in
-// registers, so the hook costs no scalar registers when timing is off).
+// Debug hooks at phase boundaries: watchdog progress, and, in the timing
+// build only (-DDPG_PHASE_TIMING: pipelinedp_amd/lib/libdpg_timing.so, loaded
+// when the env var DPG_PHASE_TIMING is set), the shader cycles thread 0 spent
+// since the previous mark, accumulated in registers and flushed once per
+// workgroup.  The product build carries no timer state at all.
+#ifdef DPG_PHASE_TIMING
 struct PhaseTimer {
     uint64_t last;
+    uint64_t pt[10];
 };
+#else
+struct PhaseTimer {};
+#endif
 __device__ __forceinline__ void mark(const BoundParams &bp, uint32_t phase, PhaseTimer &tm) {
     if (bp.progress && threadIdx.x == 0)
         __hip_atomic_store(&bp.progress[blockIdx.x], phase, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
+#ifdef DPG_PHASE_TIMING
     if (bp.phase_cyc) {
         const uint64_t now = __builtin_amdgcn_s_memtime();
-        if (threadIdx.x == 0) atomicAdd(&bp.phase_cyc[phase], (unsigned long long)(now - tm.last));
+        tm.pt[phase] += now - tm.last;
         tm.last = now;
     }
+#else
+    (void)phase;
+    (void)tm;
+#endif
 }
 __device__ __forceinline__ void timer_start(const BoundParams &bp, PhaseTimer &tm) {
+#ifdef DPG_PHASE_TIMING
     tm.last = bp.phase_cyc ? __builtin_amdgcn_s_memtime() : 0;
+    for (int k = 0; k < 10; ++k) tm.pt[k] = 0;
+#else
+    (void)bp;
+    (void)tm;
+#endif
 }
-__device__ __forceinline__ void timer_flush(const BoundParams &, const PhaseTimer &) {}
+__device__ __forceinline__ void timer_flush(const BoundParams &bp, const PhaseTimer &tm) {
+#ifdef DPG_PHASE_TIMING
+    if (bp.phase_cyc && threadIdx.x == 0)
+        for (int k = 0; k < 10; ++k) atomicAdd(&bp.phase_cyc[k], (unsigned long long)tm.pt[k]);
+#else
+    (void)bp;
+    (void)tm;
+#endif
+}
 
 __host__ __device__ __forceinline__ uint32_t next_pow2(uint32_t x) {
     uint32_t p = 64;

@@ -226,14 +226,15 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
     const uint32_t hshift = f.kbits - f.b1;
     const uint32_t kn = (n + 63) >> 6;  // occupied record slots per lane (uniform)
 
-    // ---- A: pair inserts: home-slot CAS of all records in flight, then
-    // linear probing of the colliding ones, one probe step of all of them per
-    // round (table load <= 1/2)
+    // ---- A: pair inserts: home-slot CAS of all records in flight; a record
+    // whose home holds another key tries a second slot (other bits of the same
+    // hash), then probes linearly from there -- one probe step of all of them
+    // per round (table load <= 1/2; both choices taken ~ load^2)
     uint32_t qs[kWRPT], dn[kWRPT];
     uint32_t validm = 0;  // per-lane bit k
     uint32_t npair = 0, npid = 0;
     {
-        uint32_t ps[kWRPT], wonm = 0;
+        uint32_t ps[kWRPT], alt[kWRPT], wonm = 0;
         KeyT pkey[kWRPT], op[kWRPT];
 #pragma unroll
         for (int k = 0; k < kWRPT; ++k) {
@@ -242,7 +243,9 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
             const uint64_t key = RecOps<R>::key(r[k], f);
             qs[k] = ((uint32_t)(key >> pkb) - hbase) & (kWCq - 1);
             pkey[k] = ((KeyT)qs[k] << pkb) | (KeyT)(key & pkmask);
-            ps[k] = hslot(pkey[k], kWCk - 1);
+            const uint32_t hh = hslot(pkey[k], 0xFFFFFFFFu);
+            ps[k] = hh & (kWCk - 1);
+            alt[k] = (hh >> 16) & (kWCk - 1);  // second choice (other hash bits)
             KeyT *tgt = valid ? keys + ps[k] : reinterpret_cast<KeyT *>(pool) + (lane + 64u * k);
             op[k] = cas_home<KeyT>(tgt, 0, pkey[k]);
         }
@@ -262,7 +265,7 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
 #pragma unroll
             for (int k = 0; k < kWRPT; ++k) {
                 if ((pend >> k) & 1u) {
-                    ps[k] = (ps[k] + 1) & (kWCk - 1);
+                    ps[k] = it == 0 ? alt[k] : (ps[k] + 1) & (kWCk - 1);
                     op[k] = cas_home<KeyT>(keys, ps[k], pkey[k]);
                 }
             }
