@@ -50,10 +50,9 @@ struct WaveLayout {
     static constexpr size_t PIDV = 0;                   // pid_hash of the privacy id
     static constexpr size_t PIDM = PIDV + 4 * kWCq;     // low 16: pairs/records, high: appends
     static constexpr size_t PIDSLOT = PIDM + 4 * kWCq;  // pool base (+ appends << 16) or kNil
-    static constexpr size_t QLIST = PIDSLOT + 4 * kWCq;
     // pair key table (kWCk slots); once every insert has settled, a slot
     // holds its pair's dense id instead of the key
-    static constexpr size_t KEYS = QLIST + 2 * kWCq;
+    static constexpr size_t KEYS = PIDSLOT + 4 * kWCq;
     static constexpr size_t PKEY = KEYS + sizeof(KeyT) * kWCk;  // dense: pair key
     static constexpr size_t PCNT = PKEY + sizeof(KeyT) * kWCp;  // dense: records
     static constexpr size_t PST = PCNT + 4 * kWCp;              // dense: state
@@ -203,7 +202,6 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
     uint32_t *pidv = reinterpret_cast<uint32_t *>(smem + L::PIDV);
     uint32_t *pidm = reinterpret_cast<uint32_t *>(smem + L::PIDM);
     uint32_t *pidslot = reinterpret_cast<uint32_t *>(smem + L::PIDSLOT);
-    uint16_t *qlist = reinterpret_cast<uint16_t *>(smem + L::QLIST);
     KeyT *keys = reinterpret_cast<KeyT *>(smem + L::KEYS);
     KeyT *pkey_d = reinterpret_cast<KeyT *>(smem + L::PKEY);
     uint32_t *pcnt = reinterpret_cast<uint32_t *>(smem + L::PCNT);
@@ -232,7 +230,7 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
     // per round (table load <= 1/2; both choices taken ~ load^2)
     uint32_t qs[kWRPT], dn[kWRPT];
     uint32_t validm = 0;  // per-lane bit k
-    uint32_t npair = 0, npid = 0;
+    uint32_t npair = 0;
     {
         uint32_t ps[kWRPT], alt[kWRPT], wonm = 0;
         KeyT pkey[kWRPT], op[kWRPT];
@@ -306,27 +304,23 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
         wave_sync();
 #pragma unroll
         for (int k = 0; k < kWRPT; ++k) dn[k] = (uint32_t)keys[ps[k]] & (kWCp - 1);
-        // counts (all in flight); the returned pid count tells the pid's
-        // first toucher (a pair's winner; any record in PER_PRIVACY_ID mode)
+        // counts: records per pair; pairs (records in PER_PRIVACY_ID mode)
+        // per pid
         const uint32_t touchm = per_pid ? validm : wonm;
-        uint32_t oldm[kWRPT];
 #pragma unroll
         for (int k = 0; k < kWRPT; ++k) {
             if ((validm >> k) & 1u) atomicAdd(&pcnt[dn[k]], 1u);
-            oldm[k] = atomicAdd(&pidm[qs[k]], (touchm >> k) & 1u);
+            if ((touchm >> k) & 1u) atomicAdd(&pidm[qs[k]], 1u);
         }
+    }
+    // pid_hash of every pid slot of the chunk's residual range: 2 per lane,
+    // no first-toucher detection (slots without a pid get a value nobody
+    // reads)
 #pragma unroll
-        for (int k = 0; k < kWRPT; ++k) {
-            const bool first = ((touchm >> k) & 1u) && oldm[k] == 0u;
-            const uint64_t bq = __ballot(first);
-            if (first) {
-                qlist[npid + lanes_below(bq)] = (uint16_t)qs[k];
-                pidv[qs[k]] = pid_hash(
-                    bp.seed,
-                    (uint64_t)(bp.pid_min + (int64_t)hk_inv((d1 << hshift) | (hbase + qs[k]), bp.hash)));
-            }
-            npid += (uint32_t)__popcll(bq);
-        }
+    for (int j = 0; j < kWQPL; ++j) {
+        const uint32_t q = lane + 64u * j;
+        pidv[q] = pid_hash(bp.seed, (uint64_t)(bp.pid_min + (int64_t)hk_inv(
+                                                                 (d1 << hshift) | (hbase + q), bp.hash)));
     }
     if (lane == 0) {
         bump[0] = 0;
@@ -335,20 +329,19 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
     const uint32_t jn = (npair + 63) >> 6;  // occupied pair slots per lane (uniform)
     wave_sync();
     mark(bp, 1, clk);
-    // ---- B: pool regions for pids over their limit
+    // ---- B: pool regions for pids over their limit (every pid slot;
+    // empty ones count 0)
     uint32_t qv[kWQPL];
 #pragma unroll
-    for (int j = 0; j < kWQPL; ++j) qv[j] = qlist[min(lane + 64u * j, npid - 1)] & (kWCq - 1);
+    for (int j = 0; j < kWQPL; ++j) qv[j] = lane + 64u * j;
     {
         uint32_t m[kWQPL];
 #pragma unroll
         for (int j = 0; j < kWQPL; ++j) m[j] = pidm[qv[j]] & 0xFFFFu;
 #pragma unroll
         for (int j = 0; j < kWQPL; ++j) {
-            const bool occ = lane + 64u * j < npid;
-            const bool want = occ && m[j] > lim;
-            const uint32_t sl = want ? atomicAdd(&bump[0], m[j]) : kNil;
-            if (occ) pidslot[qv[j]] = sl;
+            const bool want = m[j] > lim;
+            pidslot[qv[j]] = want ? atomicAdd(&bump[0], m[j]) : kNil;
         }
     }
     wave_sync();
@@ -412,8 +405,7 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
 #pragma unroll
             for (int j = 0; j < kWQPL; ++j)
                 region_thresholds(pool,
-                                  __ballot(lane + 64u * j < npid && psb[j] != kNil &&
-                                           pnc[j] >= bp.mpc),
+                                  __ballot(psb[j] != kNil && pnc[j] >= bp.mpc),
                                   psb[j], pnc[j], bp.mpc);
         }
         wave_sync();
@@ -592,7 +584,7 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
             }
 #pragma unroll
             for (int j = 0; j < kWQPL; ++j)
-                region_thresholds(pool, __ballot(lane + 64u * j < npid && psb[j] != kNil), psb[j],
+                region_thresholds(pool, __ballot(psb[j] != kNil), psb[j],
                                   pnc[j], bp.L);
         }
         wave_sync();
@@ -668,8 +660,7 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
             reinterpret_cast<uint4 *>(keys)[lane + 64u * i] = make_uint4(~0u, ~0u, ~0u, ~0u);
     }
 #pragma unroll
-    for (int j = 0; j < kWQPL; ++j)
-        if (lane + 64u * j < npid) pidm[qv[j]] = 0;
+    for (int j = 0; j < kWQPL; ++j) pidm[qv[j]] = 0;
     wave_sync();
     mark(bp, 8, clk);
     return nitems;
