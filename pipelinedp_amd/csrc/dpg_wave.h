@@ -255,26 +255,65 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
             if (op[k] == empty_key<KeyT>()) wonm |= 1u << k;
             else if (op[k] != pkey[k]) pend |= 1u << k;
         }
-        for (uint32_t it = 0; __ballot(pend != 0); ++it) {
-            if (it >= kWCk) {
-                if (pend) atomicOr(bp.err, 2u);
-                break;
-            }
+        // records whose home slot holds another key are compacted into a
+        // dense list (one per lane; the pool -- its dummy words are spent --
+        // holds the keys, the idle accumulator area the second-choice slot
+        // and the record's position) and probe there: second-choice slot,
+        // then linearly; the final slot (and whether the record created the
+        // entry) returns through the idle pair-state array by position
+        {
+            KeyT *ckey = reinterpret_cast<KeyT *>(pool);
+            uint32_t *cmeta = reinterpret_cast<uint32_t *>(acc_sum);
+            uint32_t *cres = pst;
+            uint32_t npend = 0;
 #pragma unroll
             for (int k = 0; k < kWRPT; ++k) {
-                if ((pend >> k) & 1u) {
-                    ps[k] = it == 0 ? alt[k] : (ps[k] + 1) & (kWCk - 1);
-                    op[k] = cas_home<KeyT>(keys, ps[k], pkey[k]);
+                const bool pk_ = (pend >> k) & 1u;
+                const uint64_t b = __ballot(pk_);
+                if (pk_) {
+                    const uint32_t e = npend + lanes_below(b);
+                    ckey[e] = pkey[k];
+                    cmeta[e] = alt[k] | ((lane + 64u * k) << 16);
                 }
+                npend += (uint32_t)__popcll(b);
             }
+            if (npend) {
+                wave_sync();
+                for (uint32_t e0 = 0; e0 < npend; e0 += 64) {
+                    const uint32_t e = min(e0 + lane, npend - 1);
+                    const bool act = e0 + lane < npend;
+                    const KeyT key = ckey[e];
+                    const uint32_t meta = cmeta[e];
+                    uint32_t slot = meta & 0xFFFFu;
+                    bool done = !act, won = false;
+                    for (uint32_t it = 0; __ballot(!done); ++it) {
+                        if (it >= kWCk) {
+                            if (!done) atomicOr(bp.err, 2u);
+                            break;
+                        }
+                        if (!done) {
+                            const KeyT o = cas_home<KeyT>(keys, slot, key);
+                            if (o == empty_key<KeyT>()) {
+                                won = true;
+                                done = true;
+                            } else if (o == key) {
+                                done = true;
+                            } else {
+                                slot = (slot + 1) & (kWCk - 1);
+                            }
+                        }
+                    }
+                    if (act) cres[meta >> 16] = slot | (won ? 0x8000u : 0u);
+                }
+                wave_sync();
+                uint32_t res[kWRPT];
 #pragma unroll
-            for (int k = 0; k < kWRPT; ++k) {
-                if ((pend >> k) & 1u) {
-                    if (op[k] == empty_key<KeyT>()) {
-                        wonm |= 1u << k;
-                        pend &= ~(1u << k);
-                    } else if (op[k] == pkey[k]) {
-                        pend &= ~(1u << k);
+                for (int k = 0; k < kWRPT; ++k) res[k] = cres[lane + 64u * k];
+#pragma unroll
+                for (int k = 0; k < kWRPT; ++k) {
+                    if ((pend >> k) & 1u) {
+                        ps[k] = res[k] & (kWCk - 1);
+                        if (res[k] & 0x8000u) wonm |= 1u << k;
                     }
                 }
             }
