@@ -180,6 +180,11 @@ __device__ __forceinline__ void cascade_insert(uint64_t *slots, uint32_t k, uint
 // above the threshold exceeds every candidate's), and the completion pass
 // handles the rest (candidate count < k).  The threshold only steers work:
 // the kept set does not depend on it.
+// Candidate bound for an expected e candidates among m pairs.
+__device__ __forceinline__ uint32_t cand_threshold_e(uint32_t m, float e) {
+    if (e >= (float)m) return 0xFFFFFFFFu;
+    return (uint32_t)(e / (float)m * 4294967040.0f);
+}
 __device__ __forceinline__ uint32_t cand_threshold(uint32_t m, uint32_t k) {
     const float e = (float)k + 3.0f * sqrtf((float)k) + 3.0f;
     if (e >= (float)m) return 0xFFFFFFFFu;

@@ -76,38 +76,6 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Count of keys in a[base, base + cnt) below x for every slot j with
-// cnt[j] > 0, batched across the slots: every round issues W clamped loads
-// per slot before any compare, so the LDS round trips of all slots overlap.
-// Slots j >= jn (uniform) hold nothing and are skipped.
-template <int J, int W = 2>
-__device__ __forceinline__ void rank_batch(const uint64_t *pool, const uint32_t (&base)[J],
-                                           const uint32_t (&cnt)[J], const uint64_t (&x)[J],
-                                           uint32_t (&rk)[J], uint32_t jn) {
-    uint32_t mx = 0;
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-        rk[j] = 0;
-        if (j < jn) mx = max(mx, cnt[j]);
-    }
-    for (uint32_t t = 0; __ballot(t < mx); t += W) {
-        uint64_t y[J][W];
-#pragma unroll
-        for (int j = 0; j < J; ++j) {
-            if (j >= jn) continue;
-            const uint32_t last = cnt[j] ? cnt[j] - 1 : 0;
-#pragma unroll
-            for (int u = 0; u < W; ++u) y[j][u] = pool[base[j] + min(t + u, last)];
-        }
-#pragma unroll
-        for (int j = 0; j < J; ++j) {
-            if (j >= jn) continue;
-#pragma unroll
-            for (int u = 0; u < W; ++u) rk[j] += (t + u < cnt[j] && y[j][u] < x[j]) ? 1u : 0u;
-        }
-    }
-}
-
 // Threshold search over key regions of the pool.  `mask` (uniform) selects
 // lanes whose (vb, vc) describe a region [vb, vb + vc) with vc >= K keys; for
 // every such region the K-th smallest key T is found and written over the
@@ -394,11 +362,14 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
     if constexpr (!per_pid) {
         // ---- C1: candidates (priority below the pid's threshold) append
         // their pair key to the pid's region
-        uint32_t sb[kWPPL], nc[kWPPL];
+        uint32_t sb[kWPPL], m[kWPPL];
         uint64_t k64[kWPPL];
         uint32_t overm = 0, candm = 0;
+        // round-0 candidate bound: about k + 2 sqrt(k) + 2 expected
+        // candidates per pid (~1.5 % of pids need a second round)
+        const float e0 = (float)bp.mpc + 2.0f * sqrtf((float)bp.mpc) + 2.0f;
         {
-            uint32_t pv[kWPPL], m[kWPPL];
+            uint32_t pv[kWPPL];
 #pragma unroll
             for (int j = 0; j < kWPPL; ++j) {
                 const uint32_t q = (uint32_t)(pkv[j] >> pkb) & (kWCq - 1);
@@ -416,7 +387,7 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
                 const uint32_t pk = (uint32_t)(pkv[j] & (KeyT)pkmask);
                 const uint32_t pr = pair_prio_h(pv[j], pk);
                 k64[j] = ((uint64_t)pr << 32) | pk;
-                if (pr < cand_threshold(m[j], bp.mpc)) candm |= 1u << j;
+                if (pr < cand_threshold_e(m[j], e0)) candm |= 1u << j;
             }
             uint32_t pos[kWPPL];
 #pragma unroll
@@ -430,64 +401,65 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
         }
         wave_sync();
         mark(bp, 3, clk);
-        // ---- C2: with >= mpc candidates, a candidate is kept iff fewer than
-        // mpc candidates have a smaller key; with fewer (rare), every
-        // candidate is kept and the non-candidates append after them (C3)
-        // threshold of every pid with >= mpc candidates (region_thresholds)
+        // ---- C2: every pid with >= mpc candidates gets its threshold, the
+        // mpc-th smallest candidate key (every non-candidate key exceeds every
+        // candidate key); pids short of candidates widen their priority bound
+        // and append the next pairs (round 1: 4 x e0; round 2: every pair),
+        // whose keys all exceed the earlier candidates', and try again
         {
-            uint32_t psb[kWQPL], pnc[kWQPL];
+            uint32_t donem = 0;  // pid slots whose threshold is set (bit j)
+            for (uint32_t rnd = 0;; ++rnd) {
+                uint32_t psb[kWQPL], pnc[kWQPL];
 #pragma unroll
-            for (int j = 0; j < kWQPL; ++j) {
-                psb[j] = pidslot[qv[j]];
-                pnc[j] = pidm[qv[j]] >> 16;
+                for (int j = 0; j < kWQPL; ++j) {
+                    psb[j] = pidslot[qv[j]];
+                    pnc[j] = pidm[qv[j]] >> 16;
+                }
+                bool shortq = false;
+#pragma unroll
+                for (int j = 0; j < kWQPL; ++j) {
+                    const bool over = psb[j] != kNil;
+                    const bool ready = over && pnc[j] >= bp.mpc && !((donem >> j) & 1u);
+                    region_thresholds(pool, __ballot(ready), psb[j], pnc[j], bp.mpc);
+                    if (ready) donem |= 1u << j;
+                    shortq |= over && pnc[j] < bp.mpc;
+                }
+                if (!__ballot(shortq)) break;
+                wave_sync();
+                uint32_t ncp[kWPPL], pos[kWPPL], newm = 0;
+#pragma unroll
+                for (int j = 0; j < kWPPL; ++j) {
+                    const uint32_t q = (uint32_t)(pkv[j] >> pkb) & (kWCq - 1);
+                    ncp[j] = pidm[q] >> 16;
+                }
+#pragma unroll
+                for (int j = 0; j < kWPPL; ++j) {
+                    const bool over = (overm >> j) & 1u, cand = (candm >> j) & 1u;
+                    if (over && !cand && ncp[j] < bp.mpc &&
+                        (rnd > 0 || (uint32_t)(k64[j] >> 32) < cand_threshold_e(m[j], 4.0f * e0)))
+                        newm |= 1u << j;
+                }
+#pragma unroll
+                for (int j = 0; j < kWPPL; ++j) {
+                    const uint32_t q = (uint32_t)(pkv[j] >> pkb) & (kWCq - 1);
+                    pos[j] = ((newm >> j) & 1u) ? atomicAdd(&pidm[q], 1u << 16) >> 16 : 0u;
+                }
+#pragma unroll
+                for (int j = 0; j < kWPPL; ++j)
+                    if ((newm >> j) & 1u) pool[sb[j] + pos[j]] = k64[j];
+                candm |= newm;
+                wave_sync();
             }
-#pragma unroll
-            for (int j = 0; j < kWQPL; ++j)
-                region_thresholds(pool,
-                                  __ballot(psb[j] != kNil && pnc[j] >= bp.mpc),
-                                  psb[j], pnc[j], bp.mpc);
         }
         wave_sync();
         {
-            uint32_t rb[kWPPL], rc[kWPPL], rk[kWPPL];
             uint64_t thr[kWPPL];
 #pragma unroll
-            for (int j = 0; j < kWPPL; ++j) {
-                const uint32_t q = (uint32_t)(pkv[j] >> pkb) & (kWCq - 1);
-                nc[j] = ((overm >> j) & 1u) ? pidm[q] >> 16 : 0u;
-                thr[j] = pool[((overm >> j) & 1u) ? sb[j] : 0u];
-            }
-            uint32_t shortm = 0;
+            for (int j = 0; j < kWPPL; ++j) thr[j] = pool[((overm >> j) & 1u) ? sb[j] : 0u];
 #pragma unroll
             for (int j = 0; j < kWPPL; ++j) {
                 const bool over = (overm >> j) & 1u, cand = (candm >> j) & 1u;
-                const bool full = nc[j] >= bp.mpc;
-                if (over && full && !(cand && k64[j] <= thr[j])) keptm &= ~(1u << j);
-                if (over && !full && !cand) shortm |= 1u << j;
-            }
-            if (__ballot(shortm != 0)) {
-                uint32_t pos[kWPPL];
-#pragma unroll
-                for (int j = 0; j < kWPPL; ++j) {
-                    const uint32_t q = (uint32_t)(pkv[j] >> pkb) & (kWCq - 1);
-                    pos[j] = ((shortm >> j) & 1u) ? atomicAdd(&pidslot[q], 1u << 16) >> 16 : 0u;
-                }
-#pragma unroll
-                for (int j = 0; j < kWPPL; ++j)
-                    if ((shortm >> j) & 1u) pool[sb[j] + nc[j] + pos[j]] = k64[j];
-                wave_sync();
-                // C3: non-candidates of such pids rank among the appended ones
-#pragma unroll
-                for (int j = 0; j < kWPPL; ++j) {
-                    const uint32_t q = (uint32_t)(pkv[j] >> pkb) & (kWCq - 1);
-                    const bool sh = (shortm >> j) & 1u;
-                    rb[j] = sh ? sb[j] + nc[j] : 0u;
-                    rc[j] = sh ? pidslot[q] >> 16 : 0u;
-                }
-                rank_batch<kWPPL>(pool, rb, rc, k64, rk, jn);
-#pragma unroll
-                for (int j = 0; j < kWPPL; ++j)
-                    if (((shortm >> j) & 1u) && rk[j] >= bp.mpc - nc[j]) keptm &= ~(1u << j);
+                if (over && !(cand && k64[j] <= thr[j])) keptm &= ~(1u << j);
             }
         }
         wave_sync();
@@ -709,7 +681,7 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
 // (w, w + G, ...); workgroup g appends its items to items[wg_off[g], ...)
 // and leaves the count in wg_cnt[g].
 template <class KeyT, class Item, class R, bool kPerPid>
-__global__ __launch_bounds__(64) void k_bound_waves(const R *recs, const R *refined,
+__global__ __launch_bounds__(64, 2) void k_bound_waves(const R *recs, const R *refined,
                                                     const uint4 *chunks, const uint32_t *n_chunks,
                                                     BoundParams bp, Item *items,
                                                     const int64_t *wg_off, uint32_t *wg_cnt) {
