@@ -315,6 +315,49 @@ __device__ __forceinline__ uint32_t block_scan_digits_t(const uint32_t *cnt, uin
     return total;
 }
 
+// Scatter's per-sub-tile digit scan: dstart[0, F] <- exclusive prefix of
+// cnt (dstart[F] = total), and for every digit cur[d] += cnt[d], cnt[d] = 0
+// (the write-out then addresses cur[d] - dstart[d + 1] + k).  Two barriers:
+// the wave totals' buffer is next written one sub-tile later, behind the
+// caller's own barriers.
+template <int T, int DPT>
+__device__ __forceinline__ uint32_t scatter_scan_update(uint32_t *cnt, uint32_t *dstart,
+                                                        uint32_t *cur, uint32_t F,
+                                                        uint32_t *sh16) {
+    constexpr int NW = T / 64;
+    const uint32_t d0 = DPT * threadIdx.x;
+    uint32_t c[DPT], x = 0;
+#pragma unroll
+    for (int u = 0; u < DPT; ++u) {
+        c[u] = d0 + u < F ? cnt[d0 + u] : 0u;
+        x += c[u];
+    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t wt;
+    uint32_t e = wave_excl_scan(x, wt);
+    if (lane == 63) sh16[w] = wt;
+    __syncthreads();
+    uint32_t total = 0;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+        const uint32_t y = sh16[k];
+        if (k < w) e += y;
+        total += y;
+    }
+#pragma unroll
+    for (int u = 0; u < DPT; ++u) {
+        if (d0 + u < F) {
+            dstart[d0 + u] = e;
+            cur[d0 + u] += c[u];
+            cnt[d0 + u] = 0;
+        }
+        e += c[u];
+    }
+    if (threadIdx.x == 0) dstart[F] = total;
+    __syncthreads();
+    return total;
+}
+
 // grid S: base[s][d] = seg_start[s] + exclusive_prefix_d(tot[s][.])  (F <= 2048)
 __global__ __launch_bounds__(1024) void k_digit_base(const int64_t *seg_start, uint32_t F,
                                                      const uint32_t *tot, int64_t *base) {
@@ -380,7 +423,7 @@ template <class Src, class Rec, int IPT, int FMAX>
 constexpr size_t scatter_lds() {
     return (size_t)sizeof(Rec) * kScatThreads * IPT +
            (Src::kDigitFromRec ? 0 : a16((size_t)2 * kScatThreads * IPT)) + (size_t)FMAX * 12 +
-           64;
+           80;
 }
 
 // kAgg: wave-aggregated ranking (few digits) instead of one LDS atomic per
@@ -400,7 +443,7 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
     const size_t o = sizeof(Rec) * SUB + (kSD ? a16((size_t)2 * SUB) : 0);
     uint32_t *cnt = reinterpret_cast<uint32_t *>(smem + o);
     uint32_t *dstart = cnt + FMAX;
-    uint32_t *cur = dstart + FMAX;  // output positions (n < 2^32 per device)
+    uint32_t *cur = dstart + FMAX + 1;  // output positions (n < 2^32 per device)
     uint32_t *sh16 = cur + FMAX;
 
     const uint32_t t = blockIdx.x;
@@ -457,7 +500,7 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
         }
         __syncthreads();
         const uint32_t total =
-            block_scan_digits_t<kScatThreads, FMAX / kScatThreads>(cnt, dstart, F, sh16);
+            scatter_scan_update<kScatThreads, FMAX / kScatThreads>(cnt, dstart, cur, F, sh16);
 #pragma unroll
         for (int j = 0; j < IPT; ++j)
             if (dr[j] != ~0u) {
@@ -490,16 +533,13 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
 #pragma unroll
             for (int u = 0; u < WB; ++u) {
                 const uint32_t k = k0 + u * kScatThreads + tid;
-                const uint32_t dst = cur[dd[u]] - dstart[dd[u]] + k;
+                // cur already includes this sub-tile: its run ends at cur[d]
+                const uint32_t dst = cur[dd[u]] - dstart[dd[u] + 1] + k;
                 if (k < total) *reinterpret_cast<W *>(&out[dst]) = x[u];
             }
         }
-        __syncthreads();
-        for (uint32_t d = tid; d < F; d += kScatThreads) {
-            cur[d] += cnt[d];
-            cnt[d] = 0;
-        }
-        __syncthreads();
+        // the next sub-tile's first barrier (after its ranking) orders this
+        // write-out's LDS reads before the next scan and staging
     }
 }
 
