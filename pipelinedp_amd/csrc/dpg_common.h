@@ -240,17 +240,19 @@ __device__ __forceinline__ double clampd(double x, double lo, double hi) {
     return x < lo ? lo : (x > hi ? hi : x);
 }
 
-// Wave-level exclusive prefix of a per-lane count; returns the wave total.
+// Exclusive prefix sum over the 64 lanes of a wave (all lanes active) in
+// registers: DPP row shifts 1/2/4/8 scan each row of 16 lanes, then row
+// broadcasts of lanes 15 and 31 carry the row totals (gfx9 DPP).
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, uint32_t &total) {
-    uint32_t v = x;
-    const int lane = __lane_id();
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        uint32_t y = __shfl_up(v, o, 64);
-        if (lane >= o) v += y;
-    }
-    total = __shfl(v, 63, 64);
-    return v - x;
+    int v = (int)x;
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);  // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);  // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);  // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);  // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    total = (uint32_t)__builtin_amdgcn_readlane(v, 63);
+    return (uint32_t)v - x;
 }
 
 }  // namespace dpg
