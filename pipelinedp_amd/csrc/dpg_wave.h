@@ -178,7 +178,6 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
     double *acc_sum = reinterpret_cast<double *>(smem + L::ACC);
     double *acc_nsum = acc_sum + kWCp;
     double *acc_nsq = acc_nsum + kWCp;
-    uint32_t *bump = reinterpret_cast<uint32_t *>(smem + L::SH);
 
     const uint32_t lane = __lane_id();
     const Fmt f = bp.fmt;
@@ -329,10 +328,6 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
         pidv[q] = pid_hash(bp.seed, (uint64_t)(bp.pid_min + (int64_t)hk_inv(
                                                                  (d1 << hshift) | (hbase + q), bp.hash)));
     }
-    if (lane == 0) {
-        bump[0] = 0;
-        bump[1] = 0;
-    }
     const uint32_t jn = (npair + 63) >> 6;  // occupied pair slots per lane (uniform)
     wave_sync();
     mark(bp, 1, clk);
@@ -345,10 +340,15 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
         uint32_t m[kWQPL];
 #pragma unroll
         for (int j = 0; j < kWQPL; ++j) m[j] = pidm[qv[j]] & 0xFFFFu;
+        // region offsets by a wave prefix sum (registers only)
+        uint32_t run = 0;
 #pragma unroll
         for (int j = 0; j < kWQPL; ++j) {
             const bool want = m[j] > lim;
-            pidslot[qv[j]] = want ? atomicAdd(&bump[0], m[j]) : kNil;
+            uint32_t tot;
+            const uint32_t ex = wave_excl_scan(want ? m[j] : 0u, tot);
+            pidslot[qv[j]] = want ? run + ex : kNil;
+            run += tot;
         }
     }
     wave_sync();
@@ -470,10 +470,14 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
         {
 #pragma unroll
             for (int j = 0; j < kWPPL; ++j) c[j] = pcnt[lane + 64u * j];
+            uint32_t run = 0;
 #pragma unroll
             for (int j = 0; j < kWPPL; ++j) {
                 const bool need = sample && ((keptm >> j) & 1u) && c[j] > bp.mcpp;
-                b2[j] = need ? atomicAdd(&bump[1], c[j]) : kKeptAll;
+                uint32_t tot;
+                const uint32_t ex = wave_excl_scan(need ? c[j] : 0u, tot);
+                b2[j] = need ? run + ex : kKeptAll;
+                run += tot;
             }
 #pragma unroll
             for (int j = 0; j < kWPPL; ++j) {
