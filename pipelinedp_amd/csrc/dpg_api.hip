@@ -481,21 +481,44 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     HIP_TRY(hipStreamSynchronize(s));
     if (hctl.err & 2u) return fail(ctx, DPG_ERR_HIP, "internal hash-table error in bounding");
     const int64_t n_items = hctl.item_cursor;
-    const SrcSeg<Item> item_src{items, wg_pre, wg_off, G + 1, (uint32_t)kRangeBits};
     // ---- merge kept pairs per partition
     Partials po{out->rows, out->count, out->sum, out->nsum, out->nsq};
     const int64_t P = pl.P;
     const int64_t nranges = (P + kRange - 1) / kRange;
-    if (n_items > 0 && nranges <= 1024) {
-        uint32_t F = (uint32_t)std::max<int64_t>(1, nranges);
-        uint32_t bits = std::max<uint32_t>(1, bits_for(F));
+    constexpr int kItemIpt = sizeof(Item) == 16 ? 8 : 4;
+    if (n_items > 0) {
+        // partition the items by 4096-partition range: one level up to 1024
+        // ranges, else two (pk >> (12 + b2), then (pk >> 12) mod 2^b2) --
+        // the final segment index is the range id either way
+        const uint32_t rb = std::max<uint32_t>(1, bits_for((uint64_t)std::max<int64_t>(1, nranges)));
+        const uint32_t b2 = rb > 10 ? std::min<uint32_t>(kMaxB2, rb - 1) : 0u;
+        const uint32_t b1 = rb - b2;
+        const uint32_t F1 = nranges <= 1024 ? (uint32_t)std::max<int64_t>(1, nranges) : 1u << b1;
         int64_t *baseR;
         uint32_t *totR;
+        const Item *sorted;
         WS(items2, Item, "items2", n_items);
-        int r = run_level<SrcSeg<Item>, Item, (sizeof(Item) == 16 ? 8 : 4), 1024>(
-            ctx, s, item_src, 1u, nullptr, &ctl->item_cursor, nullptr, n_items, F, bits, items2,
+        const SrcSeg<Item> src1{items, wg_pre, wg_off, G + 1, (uint32_t)kRangeBits + b2};
+        int r = run_level<SrcSeg<Item>, Item, kItemIpt, 1024>(
+            ctx, s, src1, 1u, nullptr, &ctl->item_cursor, nullptr, n_items, F1, b1, items2,
             "items", &baseR, &totR, &ctl->ntiles[4]);
         if (r) return r;
+        sorted = items2;
+        uint32_t F = F1;
+        if (b2 > 0) {
+            const SrcItems<Item> src2{items2, (uint32_t)kRangeBits, (1u << b2) - 1u};
+            int64_t *base2;
+            uint32_t *tot2;
+            r = run_level<SrcItems<Item>, Item, kItemIpt, 2048>(ctx, s, src2, F1, baseR, totR,
+                                                                 nullptr, n_items, 1u << b2, b2,
+                                                                 items, "items2", &base2, &tot2,
+                                                                 &ctl->ntiles[6]);
+            if (r) return r;
+            baseR = base2;
+            totR = tot2;
+            sorted = items;
+            F = F1 << b2;
+        }
         stage(ctx, s, "reduce");
         const int64_t rtile = 65536;
         uint32_t max_tiles = (uint32_t)(n_items / rtile + F + 1);
@@ -506,11 +529,7 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
                                                       rsnt, &ctl->ntiles[5]);
         LAUNCH_CHECK();
         size_t lds_r = (size_t)kRange * (ItemTraits<Item>::var ? 3 * 8 : 8) + kRange * 8;
-        k_reduce_items<Item><<<max_tiles, 1024, lds_r, s>>>(items2, rt, &ctl->ntiles[5], P, po);
-        LAUNCH_CHECK();
-    } else if (n_items > 0) {
-        k_reduce_items_direct<Item, SrcSeg<Item>><<<ctx->n_cu * 8, 256, 0, s>>>(
-            item_src, &ctl->item_cursor, po);
+        k_reduce_items<Item><<<max_tiles, 1024, lds_r, s>>>(sorted, rt, &ctl->ntiles[5], P, po);
         LAUNCH_CHECK();
     }
     stage(ctx, s, "end");

@@ -141,6 +141,27 @@ struct SrcSeg {
     }
 };
 
+// Contiguous items (or any T with a .pk field); digit = (pk >> shift) & mask
+// (the second partition-key level of the merge).
+template <class T>
+struct SrcItems {
+    static constexpr bool kDigitFromRec = true;
+    using Raw = T;
+    const T *a;
+    uint32_t shift, mask;
+    __device__ __forceinline__ T fetch(int64_t i) const { return a[i]; }
+    __device__ __forceinline__ uint32_t digit(const T &r) const { return (r.pk >> shift) & mask; }
+    __device__ __forceinline__ bool decode(const T &x, int64_t, T &r, uint32_t &d) const {
+        r = x;
+        d = digit(x);
+        return true;
+    }
+    __device__ __forceinline__ bool hist(int64_t i, uint32_t &d) const {
+        d = digit(a[i]);
+        return true;
+    }
+};
+
 // ------------------------------------------------------------ tile table
 // One thread per segment: allocate ceil(n / tile) tiles.
 __global__ void k_build_tiles(const int64_t *seg_start, const uint32_t *seg_cnt,

@@ -238,3 +238,26 @@ def test_gpu_heavy_privacy_ids(built):
     assert np.array_equal(got["rows"], ref["rows"])
     assert np.array_equal(got["count"], ref["count"])
     assert np.allclose(got["sum"], ref["sum"], rtol=1e-9, atol=1e-9)
+
+
+@pytest.mark.parametrize("P", [6_000_000, 12_000_000], ids=["P6e6", "P1.2e7"])
+def test_gpu_large_partition_space(built, P):
+    """More than 1024 ranges of 4096 partitions: the kept pairs are merged
+    through two partition-key levels (dpg_api.hip bound_and_reduce); partials
+    equal the oracle's."""
+    rng = np.random.default_rng(31)
+    n = 300_000
+    pid = rng.integers(0, 20_000, n).astype(np.int64)
+    pk = rng.integers(0, P, n).astype(np.int64)
+    pk[: n // 3] = (rng.zipf(1.2, n // 3) - 1) % P   # some heavy partitions too
+    val = rng.uniform(0.0, 10.0, n)
+    params = pdp.AggregateParams(metrics=[pdp.Metrics.COUNT, pdp.Metrics.SUM,
+                                          pdp.Metrics.PRIVACY_ID_COUNT],
+                                 max_partitions_contributed=4, max_contributions_per_partition=2,
+                                 min_value=0.0, max_value=10.0)
+    res, _ = run_engine(pid, pk, val, params, n_partitions=P)
+    ref = oracle.bound_aggregate(pid, pk, val, res.plan.bound_fields(P), SEED)
+    got = {k: v.cpu().numpy() for k, v in res.last_partials.items() if v is not None}
+    assert np.array_equal(got["rows"], ref["rows"])
+    assert np.array_equal(got["count"], ref["count"])
+    assert np.allclose(got["sum"], ref["sum"], rtol=1e-9, atol=1e-9)
