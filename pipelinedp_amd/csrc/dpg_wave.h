@@ -117,26 +117,47 @@ __device__ __forceinline__ void region_thresholds_wide(uint64_t *pool, uint64_t 
     }
 }
 
-__device__ __forceinline__ void region_thresholds(uint64_t *pool, uint64_t mask, uint32_t vb,
-                                                  uint32_t vc, uint32_t K) {
+// sel[j] (per lane) selects the region (vb[j], vc[j]) of slot j; regions of
+// all J slots share the packed passes.
+template <int J>
+__device__ __forceinline__ void region_thresholds(uint64_t *pool, const bool (&sel)[J],
+                                                  const uint32_t (&vb)[J], const uint32_t (&vc)[J],
+                                                  uint32_t K) {
     const uint32_t lane = __lane_id();
-    const uint64_t big = mask & __ballot(vc > 64);
-    mask &= ~big;
-    while (mask) {
-        // pack regions into lanes [off, off + c)
+    uint64_t mask[J];
+    uint64_t any = 0;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        mask[j] = __ballot(sel[j]);
+        const uint64_t big = mask[j] & __ballot(vc[j] > 64);
+        mask[j] &= ~big;
+        if (big) region_thresholds_wide(pool, big, vb[j], vc[j], K);
+        any |= mask[j];
+    }
+    while (any) {
+        // pack regions into lanes [off, off + c) until the wave is full
         uint32_t my_b = 0, my_c = 0, my_off = 0, used = 0, maxc = 0;
-        for (uint64_t m = mask; m; m &= m - 1) {
-            const int l = __builtin_ctzll(m);
-            const uint32_t c = __builtin_amdgcn_readlane(vc, l);
-            if (used + c > 64) break;
-            const uint32_t b = __builtin_amdgcn_readlane(vb, l);
-            const bool inr = lane >= used && lane < used + c;
-            my_b = inr ? b : my_b;
-            my_c = inr ? c : my_c;
-            my_off = inr ? used : my_off;
-            used += c;
-            maxc = max(maxc, c);
-            mask &= ~(1ull << l);
+        bool full = false;
+        any = 0;
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            for (uint64_t m = mask[j]; m && !full; m &= m - 1) {
+                const int l = __builtin_ctzll(m);
+                const uint32_t c = __builtin_amdgcn_readlane(vc[j], l);
+                if (used + c > 64) {
+                    full = true;
+                    break;
+                }
+                const uint32_t b = __builtin_amdgcn_readlane(vb[j], l);
+                const bool inr = lane >= used && lane < used + c;
+                my_b = inr ? b : my_b;
+                my_c = inr ? c : my_c;
+                my_off = inr ? used : my_off;
+                used += c;
+                maxc = max(maxc, c);
+                mask[j] &= ~(1ull << l);
+            }
+            any |= mask[j];
         }
         const bool act = lane < used;
         const uint32_t last = my_c ? my_c - 1 : 0u;
@@ -152,7 +173,6 @@ __device__ __forceinline__ void region_thresholds(uint64_t *pool, uint64_t mask,
         // every lane of the pass has read its region: the threshold may land
         if (act && rk == K - 1) pool[my_b] = x;
     }
-    if (big) region_thresholds_wide(pool, big, vb, vc, K);
 }
 
 // Records past the chunk end hold a copy of its last record (loads are
@@ -415,15 +435,15 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
                     psb[j] = pidslot[qv[j]];
                     pnc[j] = pidm[qv[j]] >> 16;
                 }
-                bool shortq = false;
+                bool shortq = false, ready[kWQPL];
 #pragma unroll
                 for (int j = 0; j < kWQPL; ++j) {
                     const bool over = psb[j] != kNil;
-                    const bool ready = over && pnc[j] >= bp.mpc && !((donem >> j) & 1u);
-                    region_thresholds(pool, __ballot(ready), psb[j], pnc[j], bp.mpc);
-                    if (ready) donem |= 1u << j;
+                    ready[j] = over && pnc[j] >= bp.mpc && !((donem >> j) & 1u);
+                    if (ready[j]) donem |= 1u << j;
                     shortq |= over && pnc[j] < bp.mpc;
                 }
+                region_thresholds<kWQPL>(pool, ready, psb, pnc, bp.mpc);
                 if (!__ballot(shortq)) break;
                 wave_sync();
                 uint32_t ncp[kWPPL], pos[kWPPL], newm = 0;
@@ -532,9 +552,10 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
             if (sample) {
                 // threshold of every over-full kept pair; a sampled record is
                 // kept iff its key is <= the threshold
+                bool needp[kWPPL];
 #pragma unroll
-                for (int j = 0; j < kWPPL; ++j)
-                    region_thresholds(pool, __ballot(b2[j] < kKeptAll), b2[j], c[j], bp.mcpp);
+                for (int j = 0; j < kWPPL; ++j) needp[j] = b2[j] < kKeptAll;
+                region_thresholds<kWPPL>(pool, needp, b2, c, bp.mcpp);
                 wave_sync();
                 uint64_t thr[kWRPT];
 #pragma unroll
@@ -597,10 +618,10 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
                 psb[j] = pidslot[qv[j]];
                 pnc[j] = pidm[qv[j]] & 0xFFFFu;
             }
+bool overp[kWQPL];
 #pragma unroll
-            for (int j = 0; j < kWQPL; ++j)
-                region_thresholds(pool, __ballot(psb[j] != kNil), psb[j],
-                                  pnc[j], bp.L);
+            for (int j = 0; j < kWQPL; ++j) overp[j] = psb[j] != kNil;
+            region_thresholds<kWQPL>(pool, overp, psb, pnc, bp.L);
         }
         wave_sync();
         uint64_t thr[kWRPT];
