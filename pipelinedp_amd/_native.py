@@ -87,7 +87,7 @@ def load():
     with _lock:
         if _lib is not None:
             return _lib
-        path = _LIB_PATH
+        path = os.environ.get("DPG_LIB_PATH") or _LIB_PATH  # debug: A/B builds
         if os.environ.get("DPG_PHASE_TIMING"):
             # debug build with per-phase cycle counters (tools/gpu_phase.sh)
             path = _LIB_PATH.replace("libdpg.so", "libdpg_timing.so")

@@ -34,12 +34,15 @@ constexpr int kQPT = kCq / kBT;      // pid slots per thread
 constexpr int kPPT = kCp / kBT;      // pair slots per thread
 
 // small chunks: one wave each (dpg_wave.h)
-constexpr int kWCap = 512;             // records per small chunk
+#ifndef DPG_WCAP
+#define DPG_WCAP 512
+#endif
+constexpr int kWCap = DPG_WCAP;        // records per small chunk
 constexpr int kWRPT = kWCap / 64;      // records per lane
 constexpr uint32_t kWCq = 128;         // direct pid slots per small chunk
-constexpr uint32_t kWCp = 512;         // pairs (dense ids) per small chunk
+constexpr uint32_t kWCp = kWCap;       // pairs (dense ids) per small chunk
 constexpr uint32_t kWCk = 1024;        // pair key table slots (load <= 1/2)
-constexpr uint32_t kWPool = 512;       // selection keys (mpc regions, then mcpp regions)
+constexpr uint32_t kWPool = kWCap;     // selection keys (mpc regions, then mcpp regions)
 constexpr int kWQPL = kWCq / 64;       // pid slots per lane
 constexpr int kWPPL = kWCp / 64;       // pair slots per lane
 

@@ -58,10 +58,10 @@ struct WaveLayout {
     static constexpr size_t PST = PCNT + 4 * kWCp;              // dense: state
     static constexpr size_t POOL = PST + 4 * kWCp;
     static constexpr size_t ACC = POOL + 8 * kWPool;
-    static constexpr size_t SH = ACC + 8 * kWCp * (var ? 3 : 1);
+    static constexpr size_t END = ACC + 8 * kWCp * (var ? 3 : 1);
     // padded to a multiple of 4 KB so that the allocation granularity of LDS
     // cannot cost a resident wave (20 KB: 8 per CU)
-    static constexpr size_t TOTAL = (SH + 16 + 4095) & ~(size_t)4095;
+    static constexpr size_t TOTAL = (END + 4095) & ~(size_t)4095;
     static constexpr int PER_CU = (int)((160 * 1024) / TOTAL) < 16 ? (int)((160 * 1024) / TOTAL) : 16;
     static_assert(TOTAL <= 40 * 1024, "wave working set too large");
     static_assert(8 * kWPool >= sizeof(KeyT) * kWCap, "pool hosts the dummy CAS words");
@@ -329,7 +329,7 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
         }
         wave_sync();
 #pragma unroll
-        for (int k = 0; k < kWRPT; ++k) dn[k] = (uint32_t)keys[ps[k]] & (kWCp - 1);
+        for (int k = 0; k < kWRPT; ++k) dn[k] = min((uint32_t)keys[ps[k]], kWCp - 1);
         // counts: records per pair; pairs (records in PER_PRIVACY_ID mode)
         // per pid
         const uint32_t touchm = per_pid ? validm : wonm;
@@ -706,7 +706,7 @@ bool overp[kWQPL];
 // (w, w + G, ...); workgroup g appends its items to items[wg_off[g], ...)
 // and leaves the count in wg_cnt[g].
 template <class KeyT, class Item, class R, bool kPerPid>
-__global__ __launch_bounds__(64, 2) void k_bound_waves(const R *recs, const R *refined,
+__global__ __launch_bounds__(64, kWCap <= 384 ? 3 : 2) void k_bound_waves(const R *recs, const R *refined,
                                                     const uint4 *chunks, const uint32_t *n_chunks,
                                                     BoundParams bp, Item *items,
                                                     const int64_t *wg_off, uint32_t *wg_cnt) {
