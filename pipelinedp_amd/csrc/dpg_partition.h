@@ -19,6 +19,12 @@
 
 namespace dpg {
 
+#ifndef DPG_HIST_U
+#define DPG_HIST_U 8
+#endif
+#ifndef DPG_SCAT_WB
+#define DPG_SCAT_WB 8
+#endif
 constexpr int kPartThreads = 1024;  // 16 waves
 // scatter workgroups (512 threads with twice the records per thread measured
 // slower on the level-1 scatter)
@@ -202,13 +208,14 @@ __global__ __launch_bounds__(kPartThreads) void k_hist(Src src_in, const TileDes
     uint32_t *my = lh + copy * F;
     Src src = src_in;  // per-thread copy (sources may cache lookup state)
     int64_t i = td.begin + tid;
-    for (; i + 3 * kPartThreads < td.end; i += 4 * kPartThreads) {
-        uint32_t d[4];
-        bool ok[4];
+    constexpr int U = DPG_HIST_U;  // loads per thread in flight per round
+    for (; i + (U - 1) * kPartThreads < td.end; i += U * kPartThreads) {
+        uint32_t d[U];
+        bool ok[U];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) ok[u] = src.hist(i + u * kPartThreads, d[u]);
+        for (int u = 0; u < U; ++u) ok[u] = src.hist(i + u * kPartThreads, d[u]);
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+        for (int u = 0; u < U; ++u)
             if (ok[u]) atomicAdd(&my[d[u]], 1u);
     }
     for (; i < td.end; i += kPartThreads) {
@@ -540,7 +547,7 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
         }
         // write-out in batches of WB staged records per thread: the LDS reads
         // of a batch are in flight together, stores are predicated
-        constexpr int WB = IPT < 8 ? IPT : 8;
+        constexpr int WB = IPT < DPG_SCAT_WB ? IPT : DPG_SCAT_WB;
         for (uint32_t k0 = 0; k0 < total; k0 += WB * kScatThreads) {
             W x[WB];
             uint32_t dd[WB];

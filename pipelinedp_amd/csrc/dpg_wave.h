@@ -68,6 +68,10 @@ struct WaveLayout {
     static_assert(KEYS % 16 == 0, "key table cleared by 16-byte stores");
 };
 
+#ifndef DPG_E0_C
+#define DPG_E0_C 2.0f
+#endif
+
 // Compiler-level ordering of one wave's LDS accesses between phases (the
 // hardware already executes them in order).
 __device__ __forceinline__ void wave_sync() {
@@ -387,7 +391,7 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
         uint32_t overm = 0, candm = 0;
         // round-0 candidate bound: about k + 2 sqrt(k) + 2 expected
         // candidates per pid (~1.5 % of pids need a second round)
-        const float e0 = (float)bp.mpc + 2.0f * sqrtf((float)bp.mpc) + 2.0f;
+        const float e0 = (float)bp.mpc + DPG_E0_C * sqrtf((float)bp.mpc) + DPG_E0_C;
         {
             uint32_t pv[kWPPL];
 #pragma unroll

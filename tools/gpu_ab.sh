@@ -1,18 +1,23 @@
 #!/bin/bash
-# Same-box A/B: the 1e9 bench with pipelinedp_amd/lib/libdpg.so (A) and
-# $LIB_B (B), alternating, so that box-to-box variance cancels.
+# Same-box A/B: the 1e9 bench with pipelinedp_amd/lib/libdpg.so (a) and each
+# variant library in $VARIANTS (files under pipelinedp_amd/lib/), alternating
+# twice, so that box-to-box variance cancels.
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-B=${LIB_B:-pipelinedp_amd/lib/libdpg_b.so}
+VARIANTS=${VARIANTS:-libdpg_b.so}
 for i in 1 2; do
-  timeout -k 10 300 python -u bench.py --steps 4 --warmup 1 --no-cpu-baseline > gpurun_out/ab_a$i.json 2> gpurun_out/ab_a$i.err || { echo "A failed"; tail -5 gpurun_out/ab_a$i.err; exit 1; }
-  DPG_LIB_PATH=$B timeout -k 10 300 python -u bench.py --steps 4 --warmup 1 --no-cpu-baseline > gpurun_out/ab_b$i.json 2> gpurun_out/ab_b$i.err || { echo "B failed"; tail -5 gpurun_out/ab_b$i.err; exit 1; }
+  timeout -k 10 300 python -u bench.py --steps 4 --warmup 1 --no-cpu-baseline > gpurun_out/ab_a$i.json 2> gpurun_out/ab_a$i.err || { echo "a failed"; tail -5 gpurun_out/ab_a$i.err; exit 1; }
+  for v in $VARIANTS; do
+    DPG_LIB_PATH=pipelinedp_amd/lib/$v timeout -k 10 300 python -u bench.py --steps 4 --warmup 1 --no-cpu-baseline > gpurun_out/ab_${v%.so}_$i.json 2> gpurun_out/ab_${v%.so}_$i.err || { echo "$v failed"; tail -5 gpurun_out/ab_${v%.so}_$i.err; exit 1; }
+  done
 done
 python3 - <<'PY'
-import json
-for v in ("a1","b1","a2","b2"):
-    d=json.load(open(f"gpurun_out/ab_{v}.json"))
-    st=d["stage_ms"]
-    print(v, round(d["ms_per_step"],2), {k: round(st[k],2) for k in ("partition1:hist","partition1:scatter","partition2:hist","partition2:scatter","bound")})
+import glob, json, os
+for f in sorted(glob.glob("gpurun_out/ab_*.json")):
+    d = json.load(open(f))
+    st = d["stage_ms"]
+    print(os.path.basename(f)[3:-5], round(d["ms_per_step"], 2),
+          {k: round(st.get(k, 0), 2) for k in ("partition1:hist", "partition1:scatter", "partition2:hist",
+                                               "partition2:scatter", "bound")})
 PY
