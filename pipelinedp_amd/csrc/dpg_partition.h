@@ -563,6 +563,8 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
                 const uint32_t k = k0 + u * kScatThreads + tid;
                 // cur already includes this sub-tile: its run ends at cur[d]
                 const uint32_t dst = cur[dd[u]] - dstart[dd[u] + 1] + k;
+                // (non-temporal loads / stores measured slower: the partial
+                // lines of the runs merge in L2)
                 if (k < total) *reinterpret_cast<W *>(&out[dst]) = x[u];
             }
         }
