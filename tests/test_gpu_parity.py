@@ -261,3 +261,27 @@ def test_gpu_large_partition_space(built, P):
     assert np.array_equal(got["rows"], ref["rows"])
     assert np.array_equal(got["count"], ref["count"])
     assert np.allclose(got["sum"], ref["sum"], rtol=1e-9, atol=1e-9)
+
+
+def test_gpu_wide_records(built):
+    """Privacy ids spread over 2^31 values and 4e7 partitions: the packed key
+    no longer fits 64 bits, so records travel as R16; more than 7 hash bits
+    stay below a fine bucket, so every bucket takes the 256-thread chunk
+    kernel (and the refine level).  Partials equal the oracle's."""
+    rng = np.random.default_rng(77)
+    n, P = 300_000, 40_000_000
+    ids = rng.choice(np.int64(2) ** 31, 20_000, replace=False)
+    pid = ids[rng.integers(0, ids.size, n)]
+    pk = rng.integers(0, P, n).astype(np.int64)
+    pk[: n // 2] = (rng.zipf(1.3, n // 2) - 1) % 5000
+    val = rng.uniform(-2.0, 12.0, n)
+    params = pdp.AggregateParams(metrics=[pdp.Metrics.COUNT, pdp.Metrics.SUM,
+                                          pdp.Metrics.PRIVACY_ID_COUNT],
+                                 max_partitions_contributed=3, max_contributions_per_partition=2,
+                                 min_value=0.0, max_value=10.0)
+    res, _ = run_engine(pid, pk, val, params, n_partitions=P)
+    ref = oracle.bound_aggregate(pid, pk, val, res.plan.bound_fields(P), SEED)
+    got = {k: v.cpu().numpy() for k, v in res.last_partials.items() if v is not None}
+    assert np.array_equal(got["rows"], ref["rows"])
+    assert np.array_equal(got["count"], ref["count"])
+    assert np.allclose(got["sum"], ref["sum"], rtol=1e-9, atol=1e-9)
