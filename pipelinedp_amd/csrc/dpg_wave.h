@@ -68,6 +68,9 @@ struct WaveLayout {
     static_assert(KEYS % 16 == 0, "key table cleared by 16-byte stores");
 };
 
+#ifndef DPG_RT_W
+#define DPG_RT_W 4
+#endif
 #ifndef DPG_E0_C
 #define DPG_E0_C 2.0f
 #endif
@@ -167,12 +170,13 @@ __device__ __forceinline__ void region_thresholds(uint64_t *pool, const bool (&s
         const uint32_t last = my_c ? my_c - 1 : 0u;
         const uint64_t x = pool[my_b + min(lane - my_off, last)];
         uint32_t rk = 0;
-        for (uint32_t t = 0; t < maxc; t += 4) {
-            uint64_t y[4];
+        constexpr int W = DPG_RT_W;
+        for (uint32_t t = 0; t < maxc; t += W) {
+            uint64_t y[W];
 #pragma unroll
-            for (int w = 0; w < 4; ++w) y[w] = pool[my_b + min(t + w, last)];
+            for (int w = 0; w < W; ++w) y[w] = pool[my_b + min(t + w, last)];
 #pragma unroll
-            for (int w = 0; w < 4; ++w) rk += (t + w < my_c && y[w] < x) ? 1u : 0u;
+            for (int w = 0; w < W; ++w) rk += (t + w < my_c && y[w] < x) ? 1u : 0u;
         }
         // every lane of the pass has read its region: the threshold may land
         if (act && rk == K - 1) pool[my_b] = x;
