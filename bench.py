@@ -12,6 +12,9 @@ accountant construction, aggregate(), compute_budgets(), device execution
 (bounding, merge, selection, noise, compaction) and the device sync.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--records R]
+       python bench.py --workload config4 [--public]   (BASELINE configs[3]:
+       MEAN+VARIANCE, Gaussian, Pareto(1.2) records per privacy id, mpc = 50,
+       mcpp = 4, 1e8 partitions; --public: public_partitions = range(1e8))
 """
 import argparse
 import json
@@ -36,8 +39,20 @@ def zipf_cdf(P: int, s: float, device) -> torch.Tensor:
     return c / c[-1]
 
 
-def generate(n: int, n_pid: int, P: int, rank: int, seed: int, device):
-    """Synthetic Zipf-keyed records generated on the device (untimed)."""
+def pareto_cdf(n_pid: int, alpha: float, cap: float, seed: int, device) -> torch.Tensor:
+    """Heavy-tailed records per privacy id (config 4): pid i has weight
+    min(Pareto(alpha, x_m = 1), cap), drawn once from a fixed seed."""
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    u = torch.rand(n_pid, dtype=torch.float64, generator=g, device=device)
+    w = (1.0 - u).pow(-1.0 / alpha).clamp_(max=cap)
+    c = torch.cumsum(w, 0)
+    return c / c[-1]
+
+
+def generate(n: int, n_pid: int, P: int, rank: int, seed: int, device, pid_cdf=None):
+    """Synthetic Zipf-keyed records generated on the device (untimed).
+    pid_cdf: sample privacy ids from this CDF instead of uniformly."""
     gen = torch.Generator(device=device)
     gen.manual_seed(seed * 1000 + rank)
     cdf = zipf_cdf(P, 1.1, device)
@@ -48,7 +63,12 @@ def generate(n: int, n_pid: int, P: int, rank: int, seed: int, device):
     chunk = 1 << 27
     for s in range(0, n, chunk):
         e = min(n, s + chunk)
-        pid[s:e] = torch.randint(0, n_pid, (e - s,), generator=gen, device=device) + rank * n_pid
+        if pid_cdf is None:
+            pid[s:e] = torch.randint(0, n_pid, (e - s,), generator=gen, device=device)
+        else:
+            u = torch.rand(e - s, dtype=torch.float64, generator=gen, device=device)
+            pid[s:e] = torch.searchsorted(pid_cdf, u).clamp_(max=n_pid - 1)
+        pid[s:e] += rank * n_pid
         u = torch.rand(e - s, dtype=torch.float64, generator=gen, device=device)
         r = torch.searchsorted(cdf, u).clamp_(max=P - 1)
         pk[s:e] = perm[r]
@@ -56,13 +76,20 @@ def generate(n: int, n_pid: int, P: int, rank: int, seed: int, device):
     return pid, pk, val
 
 
-def host_sample(n: int, n_pid: int, P: int, seed: int):
+def host_sample(n: int, n_pid: int, P: int, seed: int, pareto=None):
     rng = np.random.default_rng(seed)
     w = np.arange(1, P + 1, dtype=np.float64) ** -1.1
     cdf = np.cumsum(w)
     cdf /= cdf[-1]
     perm = np.random.default_rng(20250202).permutation(P)
-    pid = rng.integers(0, n_pid, n)
+    if pareto is None:
+        pid = rng.integers(0, n_pid, n)
+    else:
+        alpha, cap = pareto
+        pw = np.minimum((1.0 - rng.random(n_pid)) ** (-1.0 / alpha), cap)
+        pc = np.cumsum(pw)
+        pc /= pc[-1]
+        pid = np.minimum(np.searchsorted(pc, rng.random(n)), n_pid - 1)
     pk = perm[np.minimum(np.searchsorted(cdf, rng.random(n)), P - 1)]
     val = rng.random(n) * 10.0
     return pid, pk, val
@@ -75,7 +102,8 @@ def cpu_baseline(args, P):
     from pipelinedp_amd import combiners
     n = args.cpu_records
     n_pid = max(1, int(round(args.pids * n / args.records)))
-    pid, pk, val = host_sample(n, n_pid, P, 99)
+    pid, pk, val = host_sample(n, n_pid, P, 99,
+                               (1.2, args.pid_cap) if args.workload == "config4" else None)
     acc = pdp.NaiveBudgetAccountant(1.0, 1e-6)
     plan = combiners.CompoundPlan(make_params(args), acc)
     fields = plan.bound_fields(P)
@@ -90,6 +118,11 @@ def cpu_baseline(args, P):
 
 def make_params(args):
     import pipelinedp_amd as pdp
+    if args.workload == "config4":
+        return pdp.AggregateParams(
+            metrics=[pdp.Metrics.MEAN, pdp.Metrics.VARIANCE],
+            noise_kind=pdp.NoiseKind.GAUSSIAN, max_partitions_contributed=args.mpc,
+            max_contributions_per_partition=args.mcpp, min_value=0.0, max_value=10.0)
     return pdp.AggregateParams(
         metrics=[pdp.Metrics.COUNT, pdp.Metrics.SUM, pdp.Metrics.PRIVACY_ID_COUNT],
         noise_kind=pdp.NoiseKind.LAPLACE, max_partitions_contributed=args.mpc,
@@ -101,14 +134,28 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", choices=["config2", "config4"], default="config2")
+    ap.add_argument("--public", action="store_true",
+                    help="config4: public_partitions = range(P) instead of private selection")
     ap.add_argument("--records", type=int, default=1_000_000_000)
     ap.add_argument("--pids", type=int, default=10_000_000)
-    ap.add_argument("--partitions", type=int, default=1_000_000)
-    ap.add_argument("--mpc", type=int, default=8)
-    ap.add_argument("--mcpp", type=int, default=2)
-    ap.add_argument("--cpu-records", type=int, default=40_000_000)
+    ap.add_argument("--partitions", type=int, default=None)
+    ap.add_argument("--mpc", type=int, default=None)
+    ap.add_argument("--mcpp", type=int, default=None)
+    ap.add_argument("--pid-cap", type=float, default=1000.0,
+                    help="config4: cap of the Pareto weight of one privacy id")
+    ap.add_argument("--cpu-records", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
+    c4 = args.workload == "config4"
+    if args.partitions is None:
+        args.partitions = 100_000_000 if c4 else 1_000_000
+    if args.mpc is None:
+        args.mpc = 50 if c4 else 8
+    if args.mcpp is None:
+        args.mcpp = 4 if c4 else 2
+    if args.cpu_records is None:
+        args.cpu_records = 20_000_000 if c4 else 40_000_000
 
     import pipelinedp_amd as pdp
 
@@ -122,7 +169,9 @@ def main():
         torch.distributed.init_process_group("nccl", device_id=dev)
         group = torch.distributed.group.WORLD
     P = args.partitions
-    pid, pk, val = generate(args.records, args.pids, P, rank, 1, dev)
+    pid_cdf = pareto_cdf(args.pids, 1.2, args.pid_cap, 4321, dev) if c4 else None
+    pid, pk, val = generate(args.records, args.pids, P, rank, 1, dev, pid_cdf)
+    del pid_cdf
     torch.cuda.synchronize()
     backend = pdp.MI355XBackend(device=local, seed=0xD1FF5EED, process_group=group)
     # the generator's privacy-id range and this rank's global record offset
@@ -132,11 +181,12 @@ def main():
                             record_id_offset=rank * args.records)
     ex = pdp.DataExtractors("pid", "pk", "value")
     params = make_params(args)
+    public = range(P) if (c4 and args.public) else None
 
     def step():
         acc = pdp.NaiveBudgetAccountant(1.0, 1e-6)
         eng = pdp.DPEngine(acc, backend)
-        res = eng.aggregate(cols, params, ex)
+        res = eng.aggregate(cols, params, ex, public_partitions=public)
         acc.compute_budgets()
         out = res.materialize(gather=False)
         return res, out
@@ -179,7 +229,8 @@ def main():
     # names brackets exactly one launch on the stream the kernels run on)
     kernels = {"bound": "k_bound_waves", "bound.medium": "k_bound_chunks",
                "partition1:scatter": "k_scatter<SrcSoAKey>",
-               "partition2:scatter": "k_scatter<SrcAoS>"}
+               "partition2:scatter": "k_scatter<SrcAoS>",
+               "bound.tail": "k_bound_big"}
     dom_stage = max(kernels, key=lambda k: stage_ms.get(k, 0.0))
     dom_kernel = kernels[dom_stage]
     dom_ms = stage_ms.get(dom_stage)
@@ -190,23 +241,31 @@ def main():
     if os.path.exists(tfile):
         try:
             tj = json.load(open(tfile))
-            if tj.get("records") == args.records:
+            if tj.get("records") == args.records and not c4:
                 traffic = tj.get("kernels", {}).get(dom_kernel)
         except Exception:
             traffic = None
+    if c4:
+        workload = (f"configs[3]: {args.records:.0e} records / {args.pids:.0e} privacy ids "
+                    f"(Pareto(1.2) records per id, weight cap {args.pid_cap:g}) / {P:.0e} "
+                    f"Zipf(1.1) partitions per GPU, MEAN+VARIANCE, Gaussian, "
+                    + ("public partitions" if public is not None else "private selection"))
+    else:
+        workload = ("configs[1]: 1e9 records / 1e7 privacy ids / 1e6 Zipf(1.1) partitions "
+                    "per GPU, COUNT+SUM+PRIVACY_ID_COUNT, private partition selection")
     line = {
         "metric": METRIC, "value": value, "unit": "records/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "f64", "data": "synthetic (device-generated Zipf keys, uniform values)",
-        "config": {"workload": "configs[1]: 1e9 records / 1e7 privacy ids / 1e6 Zipf(1.1) "
-                               "partitions per GPU, COUNT+SUM+PRIVACY_ID_COUNT, private "
-                               "partition selection",
+        "config": {"workload": workload,
                    "records_per_gpu": args.records, "privacy_ids_per_gpu": args.pids,
                    "partitions": P, "max_partitions_contributed": args.mpc,
-                   "max_contributions_per_partition": args.mcpp, "noise": "laplace",
+                   "max_contributions_per_partition": args.mcpp,
+                   "noise": "gaussian" if c4 else "laplace",
                    "epsilon": 1.0, "delta": 1e-6,
-                   "selection": "truncated_geometric", "parallelism": f"pid-sharded x{world}"},
+                   "selection": "public" if public is not None else "truncated_geometric",
+                   "parallelism": f"pid-sharded x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                      "traffic": traffic, "kernel": dom_kernel,

@@ -124,6 +124,29 @@ def _encode_keys(values, device, extra=None):
     return ids, table, (None if extra is None else inv[n:])
 
 
+def _public_id_tensor(public_partitions, device) -> Optional[torch.Tensor]:
+    """Integer public partitions given as a range, ndarray or tensor, as a
+    device int64 tensor (None for other containers, which are listed)."""
+    if isinstance(public_partitions, range):
+        r = public_partitions
+        return torch.arange(r.start, r.stop, r.step, dtype=torch.int64, device=device)
+    if isinstance(public_partitions, (torch.Tensor, np.ndarray)) and _integer_like(public_partitions):
+        return _to_tensor(public_partitions, device).to(torch.int64).reshape(-1)
+    return None
+
+
+def _device_bitmap(ids: torch.Tensor, P: int, device) -> Tuple[torch.Tensor, int]:
+    """Bitmap of P bits (bit i of byte i >> 3 = partition i public) built on
+    the device, and the number of distinct in-range ids."""
+    ids = ids[(ids >= 0) & (ids < P)]
+    flags = torch.zeros(((P + 7) // 8) * 8, dtype=torch.uint8, device=device)
+    flags[ids] = 1
+    count = int(flags.sum(dtype=torch.int64).item())
+    w = torch.tensor([1, 2, 4, 8, 16, 32, 64, 128], dtype=torch.uint8, device=device)
+    mask = (flags.view(-1, 8) * w).sum(1, dtype=torch.uint8)
+    return mask.contiguous(), count
+
+
 def _range(t: torch.Tensor):
     if t.numel() == 0:
         return 0, -1
@@ -155,7 +178,13 @@ def encode(col, extractors, device: torch.device, need_values: bool,
         raise ValueError("value_extractor must be set for SUM, MEAN and VARIANCE")
 
     # ---- partition keys -> dense ids
-    public_list = None if public_partitions is None else list(public_partitions)
+    # dense integer keys with a declared P and array-like public partitions:
+    # the public bitmap is built on the device (config 4: 1e8 public ids)
+    pub_dense = None
+    if public_partitions is not None and hint is not None and _integer_like(pk):
+        pub_dense = _public_id_tensor(public_partitions, device)
+    public_list = (None if public_partitions is None or pub_dense is not None
+                   else list(public_partitions))
     key_table = None
     pk_ids = None
     public_ids = None
@@ -221,7 +250,9 @@ def encode(col, extractors, device: torch.device, need_values: bool,
     enc = EncodedInput(pid=pid_ids, pk=pk_ids.contiguous(), value=val, n=n,
                        n_partitions=int(P), key_table=key_table, pid_min=pid_min,
                        pid_count=pid_count, rec_id_offset=rec_off)
-    if public_ids is not None:
+    if pub_dense is not None:
+        enc.public_mask, enc.public_count = _device_bitmap(pub_dense, int(P), device)
+    elif public_ids is not None:
         mask = np.zeros((P + 7) // 8, dtype=np.uint8)
         ids = np.unique(np.asarray(public_ids, dtype=np.int64))
         ids = ids[(ids >= 0) & (ids < P)]

@@ -401,8 +401,8 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     const bool timing = std::getenv("DPG_PHASE_TIMING") != nullptr;
     bpl.phase_cyc = nullptr;
     if (timing) {
-        WS(pc, unsigned long long, "bound.phase_cyc", 32);
-        HIP_TRY(hipMemsetAsync(pc, 0, 32 * 8, s));
+        WS(pc, unsigned long long, "bound.phase_cyc", 48);
+        HIP_TRY(hipMemsetAsync(pc, 0, 48 * 8, s));
         bpl.phase_cyc = pc;
     }
     (void)hipFuncSetAttribute((const void *)wave_kern,
@@ -466,7 +466,7 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
         BoundParams bpg = bp;
         uint32_t *gprog = watchdog_seconds() ? watchdog_buffer(n_global) : nullptr;
         bpg.progress = gprog;
-        bpg.phase_cyc = nullptr;
+        bpg.phase_cyc = timing ? bpl.phase_cyc + 32 : nullptr;
         if (watchdog_seconds())
             std::fprintf(stderr, "[dpg] %u oversize buckets, scratch %zu bytes\n", n_global, total);
         k_bound_big<Item, R><<<n_global, kBigThreads, 0, s>>>(g_base, g_start, g_cnt, g_d1, doff,
@@ -474,6 +474,23 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
                                                               wg_cnt + G);
         LAUNCH_CHECK();
         if (gprog) watchdog_wait(s, gprog, n_global, "k_bound_big");
+        if (timing) {
+            unsigned long long h[8];
+            HIP_TRY(hipMemcpy(h, bpl.phase_cyc + 32, sizeof(h), hipMemcpyDeviceToHost));
+            static const char *nmb[8] = {"clear", "A.insert", "B.slots", "C.mpc", "D.state",
+                                         "E.mcpp", "F.acc", "G.emit"};
+            unsigned long long tot = 0;
+            for (int i = 0; i < 8; ++i) tot += h[i];
+            size_t recs_big = 0;
+            uint32_t nmax = 0;
+            for (uint32_t i = 0; i < n_global; ++i) recs_big += cnt[i], nmax = std::max(nmax, cnt[i]);
+            std::fprintf(stderr, "[dpg phase] big buckets=%u records=%zu max=%u per-WG Mcycles:",
+                         n_global, recs_big, nmax);
+            for (int i = 0; i < 8; ++i)
+                std::fprintf(stderr, " %s=%.3f(%.0f%%)", nmb[i], h[i] / 1e6 / n_global,
+                             100.0 * h[i] / (tot ? tot : 1));
+            std::fprintf(stderr, "\n");
+        }
     }
     k_scan_small<<<1, 1024, 0, s>>>(wg_cnt, G + 1, wg_pre, &ctl->item_cursor);
     LAUNCH_CHECK();

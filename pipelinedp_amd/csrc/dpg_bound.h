@@ -140,6 +140,18 @@ __device__ __forceinline__ uint32_t insert_key(K *keys, uint32_t mask, K key, bo
                                                uint32_t *err) {
     uint32_t h = hslot(key, mask);
     for (uint32_t probe = 0; probe <= mask; ++probe) {
+        // a slot goes empty -> key once: a key seen by a plain load is final,
+        // so the records of a heavy privacy id (thousands on one slot) hit
+        // without serialising on its L2 line; an empty or stale view CASes
+        const K seen = __hip_atomic_load(&keys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (seen == key) {
+            won = false;
+            return h;
+        }
+        if (seen != empty_key<K>()) {
+            h = (h + 1) & mask;
+            continue;
+        }
         K old;
         if constexpr (sizeof(K) == 8)
             old = (K)atomicCAS((unsigned long long *)&keys[h], (unsigned long long)empty_key<K>(),
@@ -163,6 +175,10 @@ __device__ __forceinline__ uint32_t insert_key(K *keys, uint32_t mask, K key, bo
 
 // keep-the-k-smallest-distinct cascade (slot values only decrease)
 __device__ __forceinline__ void cascade_insert(uint64_t *slots, uint32_t k, uint64_t x) {
+    // slot values only decrease: a key above the current k-th smallest can
+    // never enter (most records of a heavy pair stop at this load)
+    if (x > __hip_atomic_load(&slots[k - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+        return;
     for (uint32_t j = 0; j < k; ++j) {
         uint64_t old = atomicMin((unsigned long long *)&slots[j], (unsigned long long)x);
         if (old == x) return;
@@ -210,15 +226,18 @@ __device__ __forceinline__ uint32_t wave_alloc(T *ctr, bool want, uint32_t per =
 // Buckets beyond the LDS chunk capacity (a privacy id with thousands of
 // records): one 1024-thread workgroup per bucket, working set in global
 // memory.  The tables are written by L2 atomics and plain stores and re-read
-// by plain loads, so each wave drops this CU's possibly stale L1 lines after
-// every barrier (agent-scope acquire, MI355X_MICROARCH.md "inter-workgroup
-// visibility").
+// by plain loads of the same workgroup, i.e. of one CU, whose XCD L2 is the
+// coherence point: every wave drains its memory operations before the
+// barrier and drops this CU's possibly stale L1 lines after it (buffer_inv
+// sc0, ~100 cycles).  An agent-scope release here would write back the whole
+// XCD L2 at every phase of every bucket (buffer_wbl2 sc1): config 4's 1e5
+// heavy privacy ids spent 458 ms in this kernel that way.
 constexpr int kBigThreads = 1024;
 
 __device__ __forceinline__ void big_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("buffer_inv sc0" ::: "memory");
 }
 
 struct BigLayout {
@@ -284,7 +303,8 @@ __global__ __launch_bounds__(kBigThreads) void k_bound_big(
     const bool sample = bp.mode == DPG_MODE_CROSS_AND_PER_PARTITION && need_v;
     const bool part_clip = bp.sum_mode == DPG_SUM_CLIP_PARTITION;
     const uint32_t lim = per_pid ? bp.L : bp.mpc;
-
+    PhaseTimer clk;
+    timer_start(bp, clk);
     // ---- clear
     for (uint32_t i = tid; i < Cq; i += kBigThreads) {
         pidtab[i] = kEmpty32;
@@ -306,6 +326,7 @@ __global__ __launch_bounds__(kBigThreads) void k_bound_big(
         sh_bump2 = n;
     }
     big_sync();
+    mark(bp, 0, clk);
     // ---- A: inserts and counts
     for (uint32_t i = tid; i < n; i += kBigThreads) {
         const uint64_t key = RecOps<R>::key(rb[i], f);
@@ -322,6 +343,7 @@ __global__ __launch_bounds__(kBigThreads) void k_bound_big(
         rps[i] = ps;
     }
     big_sync();
+    mark(bp, 1, clk);
     // ---- B: cascade slots for pids over their limit
     for (uint32_t q = tid; q < Cq; q += kBigThreads) {
         const bool occ = pidtab[q] != kEmpty32;
@@ -335,6 +357,7 @@ __global__ __launch_bounds__(kBigThreads) void k_bound_big(
         }
     }
     big_sync();
+    mark(bp, 2, clk);
     if (!per_pid) {
         // ---- C: mpc selection over pairs (candidates, then completion)
         for (uint32_t pass = 0; pass < 2; ++pass) {
@@ -357,6 +380,7 @@ __global__ __launch_bounds__(kBigThreads) void k_bound_big(
             }
             big_sync();
         }
+        mark(bp, 3, clk);
         // ---- D: pair state + mcpp slots
         for (uint32_t p = tid; p < Cp; p += kBigThreads) {
             const uint64_t pkey = pairtab[p];
@@ -377,6 +401,7 @@ __global__ __launch_bounds__(kBigThreads) void k_bound_big(
             pairst[p] = st;
         }
         big_sync();
+        mark(bp, 4, clk);
         // ---- E: mcpp cascade over record keys of over-full kept pairs
         if (sample) {
             for (uint32_t i = tid; i < n; i += kBigThreads) {
@@ -391,6 +416,7 @@ __global__ __launch_bounds__(kBigThreads) void k_bound_big(
             }
             big_sync();
         }
+        mark(bp, 5, clk);
         // ---- F: accumulators of kept records
         if (need_v) {
             for (uint32_t i = tid; i < n; i += kBigThreads) {
@@ -449,6 +475,7 @@ __global__ __launch_bounds__(kBigThreads) void k_bound_big(
         }
         big_sync();
     }
+    mark(bp, 6, clk);
     // ---- G: emit kept pairs
     Item *out = items + *item_off;
     for (uint32_t p = tid; p < Cp; p += kBigThreads) {
@@ -476,6 +503,8 @@ __global__ __launch_bounds__(kBigThreads) void k_bound_big(
         }
         out[atomicAdd(item_cursor, 1u)] = it;
     }
+    mark(bp, 7, clk);
+    timer_flush(bp, clk);
 }
 
 }  // namespace dpg

@@ -9,6 +9,9 @@ selection request (:322-323), the explain-report stages, a lazy result,
 """
 from typing import Optional
 
+import numpy as np
+import torch
+
 from pipelinedp_amd import aggregate_params as agg
 from pipelinedp_amd import budget_accounting
 from pipelinedp_amd import combiners
@@ -16,6 +19,15 @@ from pipelinedp_amd import data_extractors as dex
 from pipelinedp_amd import device_aggregate
 from pipelinedp_amd import pipeline_backend
 from pipelinedp_amd import report_generator
+
+
+def _as_collection(public_partitions):
+    """Public partitions as a re-iterable collection: ranges, arrays and
+    tensors stay as they are (the device builds their bitmap), anything else
+    (e.g. a generator) is listed."""
+    if isinstance(public_partitions, (range, list, tuple, np.ndarray, torch.Tensor)):
+        return public_partitions
+    return list(public_partitions)
 
 
 def _check_col(col):
@@ -103,7 +115,7 @@ class DPEngine:
         l0 = params.max_partitions_contributed or params.max_contributions
         return device_aggregate.DeviceAggregation(
             self._backend, col, data_extractors, plan,
-            public_partitions=None if not public else list(public_partitions),
+            public_partitions=None if not public else _as_collection(public_partitions),
             selection_spec=spec, strategy=params.partition_selection_strategy,
             max_partitions_contributed=l0, pre_threshold=params.pre_threshold,
             max_rows_per_privacy_id=max_rows,

@@ -40,3 +40,22 @@ def test_public_bitmap():
                           public_partitions=[0, 2, 9])
     bits = np.unpackbits(enc.public_mask.numpy(), bitorder="little")[:enc.n_partitions]
     assert np.nonzero(bits)[0].tolist() == [0, 2, 9]
+
+
+def test_public_bitmap_from_range_array_and_tensor_matches_list():
+    # declared P: array-like public partitions take the device-bitmap path
+    col = pdp.ColumnarData(pid=np.array([1, 2]), pk=np.array([2, 40]), value=np.array([0.0, 1.0]),
+                           n_partitions=45)
+    ex = pdp.DataExtractors("pid", "pk", "value")
+    ids = [0, 3, 8, 9, 17, 40, 44, 44, 50, -1]  # duplicates and out-of-range ids
+    ref = columnar.encode(col, ex, CPU, True, public_partitions=ids)
+    for pub in (np.array(ids), torch.tensor(ids), range(0, 45, 3)):
+        enc = columnar.encode(col, ex, CPU, True, public_partitions=pub)
+        if isinstance(pub, range):
+            want = list(pub)
+        else:
+            want = sorted({i for i in ids if 0 <= i < 45})
+            assert torch.equal(enc.public_mask, ref.public_mask)
+        bits = np.unpackbits(enc.public_mask.numpy(), bitorder="little")[:45]
+        assert np.nonzero(bits)[0].tolist() == want
+        assert enc.public_count == len(want)
