@@ -237,11 +237,11 @@ def main():
     achieved = algo_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms else None
     path_achieved = algo_bytes / (path_ms * 1e-3) / 1e9 if path_ms else None
     traffic = None
-    tfile = os.path.join(ROOT, "profiles", "hbm_traffic.json")
+    tfile = os.path.join(ROOT, "profiles", "hbm_traffic_c4.json" if c4 else "hbm_traffic.json")
     if os.path.exists(tfile):
         try:
             tj = json.load(open(tfile))
-            if tj.get("records") == args.records and not c4:
+            if tj.get("records") == args.records:
                 traffic = tj.get("kernels", {}).get(dom_kernel)
         except Exception:
             traffic = None
@@ -272,7 +272,7 @@ def main():
                      "kernel_ms": dom_ms,
                      "note": "achieved = 24 B/record x records / the dominant kernel's time "
                              "(HIP events on its stream); traffic = PMC HBM bytes per launch "
-                             "of it (FETCH_SIZE x2 + WRITE_SIZE, profiles/hbm_traffic.json)"},
+                             "of it (FETCH_SIZE x2 + WRITE_SIZE, profiles/hbm_traffic[_c4].json)"},
         "path_roofline": {"achieved": path_achieved, "frac":
                           (path_achieved / HBM_PEAK_GBS) if path_achieved else None,
                           "ms": path_ms,
