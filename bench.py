@@ -9,16 +9,21 @@ configs[2]); the partials are merged with one RCCL reduce-scatter.
 
 A step = one full DPEngine.aggregate call on resident inputs: engine +
 accountant construction, aggregate(), compute_budgets(), device execution
-(bounding, merge, selection, noise, compaction) and the device sync.
+(bounding, merge, selection, noise, compaction) and the device sync.  Every
+step is a fresh release (fresh nonce).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--records R]
        python bench.py --workload config4 [--public]   (BASELINE configs[3]:
        MEAN+VARIANCE, Gaussian, Pareto(1.2) records per privacy id, mpc = 50,
        mcpp = 4, 1e8 partitions; --public: public_partitions = range(1e8))
+--gpus N without a torch.distributed launcher re-launches itself as N ranks
+(torch.distributed.run, 127.0.0.1) before touching any GPU.
 """
 import argparse
+import hashlib
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -31,6 +36,14 @@ sys.path.insert(0, ROOT)
 METRIC = "records/sec DPEngine.aggregate COUNT+SUM at 1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0
 ALGO_BYTES_PER_RECORD = 24  # pid int64 + pk int64 + value f64
+CPU_SHARE = 16              # host cores of one GPU's share on the GPU box
+# reference LocalBackend (stub PyDP, 1 Python thread), measured in the build
+# container (synthetic 1M-record row) -- context only
+REFERENCE_LOCAL_BACKEND = {"value": 1.13e5, "unit": "records/s", "cores": 1,
+                           "kind": "reference",
+                           "sample": "reference LocalBackend, 1e6 records / 1e4 pids / 1e3 "
+                                     "Zipf partitions, no-noise PyDP stub, build container "
+                                     "(BASELINE.md section 2); not re-run on the GPU box"}
 
 
 def zipf_cdf(P: int, s: float, device) -> torch.Tensor:
@@ -76,12 +89,20 @@ def generate(n: int, n_pid: int, P: int, rank: int, seed: int, device, pid_cdf=N
     return pid, pk, val
 
 
-def host_sample(n: int, n_pid: int, P: int, seed: int, pareto=None):
-    rng = np.random.default_rng(seed)
+def host_tables(P: int):
+    """Zipf(1.1) CDF over partition ranks and the fixed rank -> key permutation."""
     w = np.arange(1, P + 1, dtype=np.float64) ** -1.1
     cdf = np.cumsum(w)
     cdf /= cdf[-1]
-    perm = np.random.default_rng(20250202).permutation(P)
+    return cdf, np.random.default_rng(20250202).permutation(P)
+
+
+def host_sample(n: int, n_pid: int, P: int, seed: int, pareto=None, pid_lo: int = 0,
+                tables=None):
+    """The same generator on the host (numpy): privacy ids in
+    [pid_lo, pid_lo + n_pid)."""
+    rng = np.random.default_rng(seed)
+    cdf, perm = tables if tables is not None else host_tables(P)
     if pareto is None:
         pid = rng.integers(0, n_pid, n)
     else:
@@ -92,28 +113,104 @@ def host_sample(n: int, n_pid: int, P: int, seed: int, pareto=None):
         pid = np.minimum(np.searchsorted(pc, rng.random(n)), n_pid - 1)
     pk = perm[np.minimum(np.searchsorted(cdf, rng.random(n)), P - 1)]
     val = rng.random(n) * 10.0
-    return pid, pk, val
+    return pid + pid_lo, pk, val
+
+
+# ---------------------------------------------------------------- CPU baseline
+_ACC = ("rows", "count", "sum", "nsum", "nsq")
+
+
+_TABLES = None  # host_tables(P), built once before the workers fork
+
+
+def _cpu_worker(w, n, n_pid_total, k, P, pareto, fields, seed, start_evt, ready_q, out_q):
+    """One host core: generate this worker's privacy-id shard, wait for the
+    common start, bound + merge it with the C oracle (timed); returns the
+    non-zero partials (sparse, so P = 1e8 does not cross the pipe densely)."""
+    from oracle import oracle
+    lo = w * n_pid_total // k
+    hi = (w + 1) * n_pid_total // k
+    pid, pk, val = host_sample(n, hi - lo, P, 99 + w, pareto, pid_lo=lo, tables=_TABLES)
+    f = dict(fields, rec_id_offset=w * n)
+    oracle.lib()
+    ready_q.put(w)
+    start_evt.wait()
+    t0 = time.perf_counter()
+    part = oracle.bound_aggregate(pid, pk, val, f, seed)
+    nz = np.nonzero(part["rows"])[0]
+    dt = time.perf_counter() - t0
+    out_q.put((w, nz, {key: part[key][nz] for key in _ACC}, dt))
 
 
 def cpu_baseline(args, P):
-    """The C oracle (single core) on a bounded sample of the same workload."""
+    """The C oracle's FULL path on the GPU box's host cores: one process per
+    core on disjoint privacy-id shards (bounding + merge), then the merge of
+    the shards' partials and the oracle's selection + noise -- the same work
+    as one GPU step, on a bounded sample of the same generator.  Runs before
+    this process touches the GPU (forked workers)."""
+    import multiprocessing as mp
     from oracle import oracle
     import pipelinedp_amd as pdp
-    from pipelinedp_amd import combiners
-    n = args.cpu_records
-    n_pid = max(1, int(round(args.pids * n / args.records)))
-    pid, pk, val = host_sample(n, n_pid, P, 99,
-                               (1.2, args.pid_cap) if args.workload == "config4" else None)
+    from pipelinedp_amd import combiners, partition_selection
+    k = max(1, min(CPU_SHARE, os.cpu_count() or 1))
+    n_each = args.cpu_records // k
+    n_pid = max(k, int(round(args.pids * args.cpu_records / args.records)))
+    pareto = (1.2, args.pid_cap) if args.workload == "config4" else None
     acc = pdp.NaiveBudgetAccountant(1.0, 1e-6)
-    plan = combiners.CompoundPlan(make_params(args), acc)
-    fields = plan.bound_fields(P)
-    t0 = time.perf_counter()
-    oracle.bound_aggregate(pid, pk, val, fields, 5)
-    dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "records/s", "cores": 1, "kind": "port",
-            "sample": f"{n} records, {n_pid} privacy ids, {P} partitions, same generator; "
-                      f"C oracle bounding+merge only (selection/noise excluded), "
-                      f"{dt:.1f} s on one host core"}
+    params = make_params(args)
+    public = args.workload == "config4" and args.public
+    plan = combiners.CompoundPlan(params, acc)
+    sel_spec = None if public else acc.request_budget(pdp.MechanismType.GENERIC)
+    acc.compute_budgets()
+    fields = dict(plan.bound_fields(P), nonce=1)
+    global _TABLES
+    _TABLES = host_tables(P)
+    ctx = mp.get_context("fork")
+    start_evt, ready_q, out_q = ctx.Event(), ctx.Queue(), ctx.Queue()
+    procs = [ctx.Process(target=_cpu_worker, args=(w, n_each, n_pid, k, P, pareto, fields, 5,
+                                                   start_evt, ready_q, out_q))
+             for w in range(k)]
+    for p in procs:
+        p.start()
+    try:
+        for _ in range(k):
+            ready_q.get(timeout=600)
+        t0 = time.perf_counter()
+        start_evt.set()
+        tot = {key: np.zeros(P, np.int64 if key in ("rows", "count") else np.float64)
+               for key in _ACC}
+        slowest = 0.0
+        for _ in range(k):
+            w, nz, part, dt = out_q.get(timeout=1200)
+            slowest = max(slowest, dt)
+            for key in _ACC:
+                np.add.at(tot[key], nz, part[key])
+        if public:
+            sel = dict(strategy=0, max_rows_per_privacy_id=1, nonce=1)
+            mask = np.full((P + 7) // 8, 0xFF, np.uint8)
+            oracle.select_and_noise(tot, sel, plan.noise_fields(True), 5, public_mask=mask)
+        else:
+            sp = partition_selection.create_partition_selection_strategy(
+                params.partition_selection_strategy, sel_spec.eps, sel_spec.delta,
+                params.max_partitions_contributed)
+            sel = dict(strategy=sp.native_strategy, threshold=sp.threshold,
+                       noise_scale=sp.noise_scale, pre_threshold=0,
+                       max_rows_per_privacy_id=1, nonce=1)
+            oracle.select_and_noise(tot, sel, plan.noise_fields(True), 5,
+                                    keep_table=None if sp.table is None else np.asarray(sp.table))
+        dt = time.perf_counter() - t0
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    n_done = n_each * k
+    return {"value": n_done / dt, "unit": "records/s", "cores": k, "kind": "port",
+            "sample": f"{n_done:.1e} records, {n_pid} privacy ids, {P} partitions, same "
+                      f"generator (one privacy-id range per core); C oracle full path: "
+                      f"bounding+merge in {k} processes (slowest {slowest:.1f} s), merge of "
+                      f"the shards' partials, selection + noise; {dt:.1f} s wall",
+            "reference_local_backend": REFERENCE_LOCAL_BACKEND}
 
 
 def make_params(args):
@@ -127,6 +224,69 @@ def make_params(args):
         metrics=[pdp.Metrics.COUNT, pdp.Metrics.SUM, pdp.Metrics.PRIVACY_ID_COUNT],
         noise_kind=pdp.NoiseKind.LAPLACE, max_partitions_contributed=args.mpc,
         max_contributions_per_partition=args.mcpp, min_value=0.0, max_value=10.0)
+
+
+# ------------------------------------------------------------ per-stage bytes
+def stage_design_bytes(stage: str, n: int, rec: int, item: int, kept_recs: int,
+                       kept_pairs: int, P: int, n_accum: int):
+    """Design HBM bytes of one stage: what the
+    stage must move at minimum for its job, not what it measures."""
+    if stage == "pidrange":
+        return 8 * n
+    if stage == "partition1:hist":
+        return 8 * n                      # pid column
+    if stage == "partition1:scatter":
+        return (16 + rec) * n             # pid + pk in, packed record out
+    if stage in ("partition2:hist", "refine:hist"):
+        return rec * n
+    if stage in ("partition2:scatter", "refine:scatter"):
+        return 2 * rec * n
+    if stage == "bound":                  # records in, kept values gathered, items out
+        return rec * n + 8 * kept_recs + item * kept_pairs
+    if stage in ("items:hist", "items2:hist"):
+        return item * kept_pairs
+    if stage in ("items:scatter", "items2:scatter"):
+        return 2 * item * kept_pairs
+    if stage == "reduce":
+        return item * kept_pairs + 8 * n_accum * P
+    return None
+
+
+def _lib_sha() -> str:
+    from pipelinedp_amd import _native
+    with open(_native.library_path(), "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
+def _traffic(c4: bool, records: int):
+    """PMC HBM bytes per step from profiles/hbm_traffic[_c4].json -- only if
+    that file was measured on this exact libdpg.so build."""
+    tfile = os.path.join(ROOT, "profiles", "hbm_traffic_c4.json" if c4 else "hbm_traffic.json")
+    if not os.path.exists(tfile):
+        return None, "no PMC file"
+    try:
+        tj = json.load(open(tfile))
+    except Exception:
+        return None, "unreadable PMC file"
+    if tj.get("records") != records:
+        return None, "PMC file measured at another record count"
+    if tj.get("lib_sha256") != _lib_sha():
+        return None, f"PMC file measured on another build ({tj.get('lib_sha256')})"
+    return tj, os.path.relpath(tfile, ROOT)
+
+
+def _launch_ranks(n: int) -> int:
+    """Re-executes this script as n ranks under torch.distributed.run, as a
+    child process started before this process touches a GPU."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 def main():
@@ -147,6 +307,8 @@ def main():
     ap.add_argument("--cpu-records", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_launch_ranks(args.gpus))
     c4 = args.workload == "config4"
     if args.partitions is None:
         args.partitions = 100_000_000 if c4 else 1_000_000
@@ -155,13 +317,19 @@ def main():
     if args.mcpp is None:
         args.mcpp = 4 if c4 else 2
     if args.cpu_records is None:
-        args.cpu_records = 20_000_000 if c4 else 40_000_000
+        args.cpu_records = 48_000_000 if c4 else 160_000_000
 
     import pipelinedp_amd as pdp
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    # the CPU baseline runs first, before this process touches the GPU
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, args.partitions)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     group = None
@@ -203,10 +371,9 @@ def main():
     t0 = time.perf_counter()
     stage_tot = {}
     ev0.record(stream)
-    kept = 0
+    res = out = None
     for _ in range(args.steps):
         res, out = step()
-        kept = int(out.partition_ids.numel())
         for k, v in backend.ctx.stage_times().items():
             stage_tot[k] = stage_tot.get(k, 0.0) + v
     ev1.record(stream)
@@ -215,36 +382,34 @@ def main():
         torch.distributed.barrier()
     wall = time.perf_counter() - t0
     dev_ms = ev0.elapsed_time(ev1) / args.steps
-    t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    t = torch.tensor([wall, dev_ms], dtype=torch.float64, device=dev)
     if group is not None:
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-    wall = float(t.item())
+    wall, dev_ms_max = float(t[0].item()), float(t[1].item())
     ms_per_step = wall / args.steps * 1e3
     total_records = args.records * world
     value = total_records / (wall / args.steps)
+    kept = int(out.partition_ids.numel())
+    lp = res.last_partials
+    kept_pairs = int(lp["rows"].sum().item())
+    kept_recs = int(lp["count"].sum().item())
     stage_ms = {k: v / args.steps for k, v in stage_tot.items()}
     path_ms = sum(stage_ms.values())
     algo_bytes = ALGO_BYTES_PER_RECORD * args.records
-    # dominant kernel: the longest single-kernel stage (each of these stage
-    # names brackets exactly one launch on the stream the kernels run on)
-    kernels = {"bound": "k_bound_waves", "bound.medium": "k_bound_chunks",
-               "partition1:scatter": "k_scatter<SrcSoAKey>",
-               "partition2:scatter": "k_scatter<SrcAoS>",
-               "bound.tail": "k_bound_big"}
-    dom_stage = max(kernels, key=lambda k: stage_ms.get(k, 0.0))
-    dom_kernel = kernels[dom_stage]
-    dom_ms = stage_ms.get(dom_stage)
-    achieved = algo_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms else None
-    path_achieved = algo_bytes / (path_ms * 1e-3) / 1e9 if path_ms else None
-    traffic = None
-    tfile = os.path.join(ROOT, "profiles", "hbm_traffic_c4.json" if c4 else "hbm_traffic.json")
-    if os.path.exists(tfile):
-        try:
-            tj = json.load(open(tfile))
-            if tj.get("records") == args.records:
-                traffic = tj.get("kernels", {}).get(dom_kernel)
-        except Exception:
-            traffic = None
+    n_accum = 5 if c4 else 3
+    rec_bytes = 16 if c4 else 8
+    item_bytes = 32 if c4 else 16
+    # headline: the whole path (24 B/record over the device time per step)
+    achieved = algo_bytes / (dev_ms_max * 1e-3) / 1e9
+    tj, tsrc = _traffic(c4, args.records)
+    kernels = {}
+    for st, ms in stage_ms.items():
+        b = stage_design_bytes(st, args.records, rec_bytes, item_bytes, kept_recs, kept_pairs,
+                               P, n_accum)
+        kernels[st] = {"ms": round(ms, 4)}
+        if b is not None and ms > 0:
+            kernels[st].update(design_bytes=b, achieved_gbs=round(b / (ms * 1e-3) / 1e9, 1),
+                               frac=round(b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))
     if c4:
         workload = (f"configs[3]: {args.records:.0e} records / {args.pids:.0e} privacy ids "
                     f"(Pareto(1.2) records per id, weight cap {args.pid_cap:g}) / {P:.0e} "
@@ -267,21 +432,22 @@ def main():
                    "selection": "public" if public is not None else "truncated_geometric",
                    "parallelism": f"pid-sharded x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-                     "traffic": traffic, "kernel": dom_kernel,
-                     "kernel_ms": dom_ms,
-                     "note": "achieved = 24 B/record x records / the dominant kernel's time "
-                             "(HIP events on its stream); traffic = PMC HBM bytes per launch "
-                             "of it (FETCH_SIZE x2 + WRITE_SIZE, profiles/hbm_traffic[_c4].json)"},
-        "path_roofline": {"achieved": path_achieved, "frac":
-                          (path_achieved / HBM_PEAK_GBS) if path_achieved else None,
-                          "ms": path_ms,
-                          "note": "24 B/record over the whole dpg_bound_aggregate device time"},
-        "device_ms_per_step": dev_ms, "bound_aggregate_ms": path_ms, "stage_ms": stage_ms,
-        "kept_partitions": kept,
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": (tj["bytes_per_step"] if tj else None),
+                     "kernel": "whole path (dpg_bound_aggregate + select/noise + compact)",
+                     "device_ms": dev_ms_max,
+                     "note": "achieved = 24 B/record x records / device time per step (HIP "
+                             "events on the kernels' stream, max over ranks); traffic = PMC "
+                             "HBM bytes per step (FETCH_SIZE x calibrated factor + WRITE_SIZE) "
+                             f"from {tsrc}"},
+        "kernels": kernels,
+        "kept_partitions": kept, "kept_pairs": kept_pairs, "kept_records": kept_recs,
+        "lib_sha256": _lib_sha(),
     }
-    if rank == 0 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(args, P)
+    if tj:
+        line["roofline"]["traffic_by_kernel"] = tj.get("kernels")
+    if cpu is not None:
+        line["cpu_baseline"] = cpu
     if rank == 0:
         print(json.dumps(line), flush=True)
     if group is not None:

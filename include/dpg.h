@@ -113,6 +113,14 @@ typedef struct dpg_bound_params {
                                     record sampler is keyed by
                                     (pid, pk, rec_id_offset + i), so shards
                                     of one dataset sample as the whole   */
+    uint64_t nonce;              /* per-release nonce: every keyed stream of
+                                    the call uses dpg_stream_seed(ctx seed,
+                                    nonce).  Callers pass a FRESH random
+                                    nonce per release (the reference draws
+                                    fresh randomness per call,
+                                    dp_computations.py:131-133, 151-152,
+                                    pipeline_backend.py:540-544) and the
+                                    same nonce on every rank of one release */
 } dpg_bound_params;
 
 /* Dense per-partition partial accumulators (structure of arrays).
@@ -141,6 +149,8 @@ typedef struct dpg_select_params {
     int64_t pk_offset;           /* global pk id of partials index 0       */
     const uint8_t *public_mask;  /* DPG_SELECT_NONE: keep iff bit set
                                     (indexed by local partition id)        */
+    uint64_t nonce;              /* per-release nonce of the selection and
+                                    noise draws (see dpg_bound_params)      */
 } dpg_select_params;
 
 typedef struct dpg_noise_params {
@@ -165,6 +175,13 @@ dpg_ctx *dpg_ctx_create(int device, uint64_t seed);
 void dpg_ctx_destroy(dpg_ctx *ctx);
 int dpg_last_error(dpg_ctx *ctx, char *buf, size_t len);
 int dpg_set_seed(dpg_ctx *ctx, uint64_t seed);
+
+/* The 64-bit key of every keyed random stream of one release:
+ * mix64(seed ^ mix64(nonce + 0x9E3779B97F4A7C15)) with mix64 the SplitMix64
+ * finaliser.  Two releases with different nonces draw independent sampling,
+ * selection and noise; the same (seed, nonce) reproduces a release exactly
+ * (tests, and every rank of one multi-GPU release). */
+uint64_t dpg_stream_seed(uint64_t seed, uint64_t nonce);
 
 /* Tuning / testing hook: average records per fine privacy-id bucket the
  * partition levels aim for (default 256; smaller values force more levels on

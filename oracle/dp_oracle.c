@@ -92,6 +92,21 @@ static inline uint64_t rec_prio(uint64_t seed, uint64_t pid, uint32_t pk, uint64
     return ((uint64_t)h << 32) | (uint32_t)gidx;
 }
 
+/* Per-release stream seed (include/dpg.h dpg_stream_seed): SplitMix64
+ * finaliser of the context seed and the release nonce. */
+static inline uint64_t mix64(uint64_t z) {
+    z ^= z >> 30;
+    z *= 0xBF58476D1CE4E5B9ull;
+    z ^= z >> 27;
+    z *= 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return z;
+}
+
+uint64_t dpo_stream_seed(uint64_t seed, uint64_t nonce) {
+    return mix64(seed ^ mix64(nonce + 0x9E3779B97F4A7C15ull));
+}
+
 static inline double u53(uint32_t a, uint32_t b) {
     uint64_t u = (((uint64_t)a << 32) | b) >> 11;
     return ((double)u + 0.5) * 0x1.0p-53;
@@ -239,6 +254,7 @@ static int64_t sample_records(uint64_t seed, const cols_t *c, const int64_t *ord
 int dpo_bound_aggregate_ids(uint64_t seed, const int64_t *pid, const int64_t *pk,
                             const double *v, const int64_t *rec_ids, int64_t n,
                             const dpg_bound_params *p, dpg_partials *out) {
+    seed = dpo_stream_seed(seed, p->nonce);
     cols_t c = {pid, pk, v, rec_ids, p->rec_id_offset};
     for (int64_t i = 0; i < n; ++i) {
         if (pk[i] < 0 || pk[i] >= p->n_partitions) return DPG_ERR_KEY_RANGE;
@@ -398,6 +414,7 @@ void dpo_partition_metrics(const dpg_noise_params *z, uint64_t seed,
 int dpo_select_and_noise(uint64_t seed, const dpg_partials *in,
                          const dpg_select_params *s, const dpg_noise_params *z,
                          uint8_t *keep, double *out) {
+    seed = dpo_stream_seed(seed, s->nonce);
     int64_t P = in->n_partitions;
     for (int64_t k = 0; k < P; ++k) {
         uint64_t gk = (uint64_t)(k + s->pk_offset);
@@ -416,7 +433,7 @@ int dpo_select_and_noise(uint64_t seed, const dpg_partials *in,
     return DPG_OK;
 }
 
-/* exported helpers for distribution tests */
+/* exported helpers for distribution tests (`seed` = the stream seed) */
 uint32_t dpo_pair_prio(uint64_t seed, uint64_t pid, uint32_t pk) {
     return pair_prio(seed, pid, pk);
 }

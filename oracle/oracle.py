@@ -24,7 +24,7 @@ class _Bound(ctypes.Structure):
                 ("max_sum_per_partition", ctypes.c_double),
                 ("n_partitions", ctypes.c_int64), ("public_mask", ctypes.c_void_p),
                 ("pid_min", ctypes.c_int64), ("pid_count", ctypes.c_int64),
-                ("rec_id_offset", ctypes.c_int64)]
+                ("rec_id_offset", ctypes.c_int64), ("nonce", ctypes.c_uint64)]
 
 
 class _Partials(ctypes.Structure):
@@ -38,7 +38,8 @@ class _Select(ctypes.Structure):
                 ("keep_table", ctypes.c_void_p), ("threshold", ctypes.c_double),
                 ("noise_scale", ctypes.c_double), ("pre_threshold", ctypes.c_int64),
                 ("max_rows_per_privacy_id", ctypes.c_int64),
-                ("pk_offset", ctypes.c_int64), ("public_mask", ctypes.c_void_p)]
+                ("pk_offset", ctypes.c_int64), ("public_mask", ctypes.c_void_p),
+                ("nonce", ctypes.c_uint64)]
 
 
 class _Noise(ctypes.Structure):
@@ -88,6 +89,8 @@ def lib():
                                            ctypes.POINTER(_Select), ctypes.POINTER(_Noise),
                                            vp, vp]
         L.dpo_select_and_noise.restype = ctypes.c_int
+        L.dpo_stream_seed.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
+        L.dpo_stream_seed.restype = ctypes.c_uint64
         L.dpo_pair_prio.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32]
         L.dpo_pair_prio.restype = ctypes.c_uint32
         L.dpo_rec_prio.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
@@ -158,6 +161,11 @@ def select_and_noise(partials: dict, select: dict, noise: dict, seed: int,
     if st != 0:
         raise ValueError(f"oracle select_and_noise failed with status {st}")
     return keep, out[:P * z.n_outputs].reshape(P, z.n_outputs)
+
+
+def stream_seed(seed, nonce):
+    return int(lib().dpo_stream_seed(ctypes.c_uint64(seed & (2**64 - 1)),
+                                     ctypes.c_uint64(nonce & (2**64 - 1))))
 
 
 def pair_prio(seed, pid, pk):

@@ -17,7 +17,7 @@ ERRORS = {1: "invalid argument", 2: "key out of range", 3: "HIP error",
 EXPORTED = ("dpg_ctx_create", "dpg_ctx_destroy", "dpg_last_error", "dpg_set_seed",
             "dpg_set_tuning",
             "dpg_bound_aggregate", "dpg_select_and_noise", "dpg_compact_kept",
-            "dpg_last_stage_times")
+            "dpg_last_stage_times", "dpg_stream_seed")
 
 
 class BoundParams(ctypes.Structure):
@@ -31,7 +31,7 @@ class BoundParams(ctypes.Structure):
                 ("max_sum_per_partition", ctypes.c_double),
                 ("n_partitions", ctypes.c_int64), ("public_mask", ctypes.c_void_p),
                 ("pid_min", ctypes.c_int64), ("pid_count", ctypes.c_int64),
-                ("rec_id_offset", ctypes.c_int64)]
+                ("rec_id_offset", ctypes.c_int64), ("nonce", ctypes.c_uint64)]
 
 
 class Partials(ctypes.Structure):
@@ -45,7 +45,8 @@ class SelectParams(ctypes.Structure):
                 ("keep_table", ctypes.c_void_p), ("threshold", ctypes.c_double),
                 ("noise_scale", ctypes.c_double), ("pre_threshold", ctypes.c_int64),
                 ("max_rows_per_privacy_id", ctypes.c_int64),
-                ("pk_offset", ctypes.c_int64), ("public_mask", ctypes.c_void_p)]
+                ("pk_offset", ctypes.c_int64), ("public_mask", ctypes.c_void_p),
+                ("nonce", ctypes.c_uint64)]
 
 
 class NoiseParams(ctypes.Structure):
@@ -106,6 +107,8 @@ def load():
         lib.dpg_last_error.restype = ctypes.c_int
         lib.dpg_set_seed.argtypes = [vp, ctypes.c_uint64]
         lib.dpg_set_seed.restype = ctypes.c_int
+        lib.dpg_stream_seed.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
+        lib.dpg_stream_seed.restype = ctypes.c_uint64
         lib.dpg_set_tuning.argtypes = [vp, i32, i32]
         lib.dpg_set_tuning.restype = ctypes.c_int
         lib.dpg_bound_aggregate.argtypes = [vp, vp, vp, vp, i64,
@@ -125,6 +128,12 @@ def load():
         lib.dpg_last_stage_times.restype = ctypes.c_int
         _lib = lib
         return lib
+
+
+def stream_seed(seed: int, nonce: int) -> int:
+    """dpg_stream_seed: the key of every random stream of one release."""
+    return int(load().dpg_stream_seed(ctypes.c_uint64(seed & (2**64 - 1)),
+                                      ctypes.c_uint64(nonce & (2**64 - 1))))
 
 
 class Context:

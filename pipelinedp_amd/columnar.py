@@ -69,6 +69,7 @@ class EncodedInput:
     pid_min: int = 0
     pid_count: int = 0        # 0: unknown (the device reduces min / max)
     rec_id_offset: int = 0
+    partitions_declared: bool = False  # dense ids in [0, n_partitions) given by the caller
 
 
 def _extract(col, extractor):
@@ -249,7 +250,8 @@ def encode(col, extractors, device: torch.device, need_values: bool,
 
     enc = EncodedInput(pid=pid_ids, pk=pk_ids.contiguous(), value=val, n=n,
                        n_partitions=int(P), key_table=key_table, pid_min=pid_min,
-                       pid_count=pid_count, rec_id_offset=rec_off)
+                       pid_count=pid_count, rec_id_offset=rec_off,
+                       partitions_declared=hint is not None and key_table is None)
     if pub_dense is not None:
         enc.public_mask, enc.public_count = _device_bitmap(pub_dense, int(P), device)
     elif public_ids is not None:

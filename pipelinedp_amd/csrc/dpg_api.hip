@@ -586,7 +586,7 @@ int pipeline(dpg_ctx *ctx, hipStream_t s, const int64_t *pid, const int64_t *pk,
         cur = recB;
         B = F1 * F2;
     }
-    BoundParams bp = to_bound(p, ctx->seed);
+    BoundParams bp = to_bound(p, stream_seed(ctx->seed, p->nonce));
     bp.fmt = f;
     bp.hash = H;
     bp.pid_min = pid_min;
@@ -638,6 +638,8 @@ int dpg_set_seed(dpg_ctx *c, uint64_t seed) {
     c->seed = seed;
     return DPG_OK;
 }
+
+uint64_t dpg_stream_seed(uint64_t seed, uint64_t nonce) { return stream_seed(seed, nonce); }
 
 int dpg_set_tuning(dpg_ctx *ctx, int32_t bucket_target, int32_t bucket_cap) {
     if (!ctx) return DPG_ERR_INVALID_ARG;
@@ -785,7 +787,9 @@ int dpg_select_and_noise(dpg_ctx *ctx, const dpg_partials *in, const dpg_select_
     int64_t blocks = std::min<int64_t>((P + threads - 1) / threads, (int64_t)ctx->n_cu * 16);
     size_t lds = (a.table && a.table_len <= 4096) ? (size_t)a.table_len * 8 : 0;
     k_select_noise<<<(unsigned)blocks, threads, lds, s>>>(in->rows, in->count, in->sum, in->nsum,
-                                                         in->nsq, P, a, na, ctx->seed, keep, out);
+                                                         in->nsq, P, a, na,
+                                                         stream_seed(ctx->seed, sel->nonce), keep,
+                                                         out);
     LAUNCH_CHECK();
     return DPG_OK;
 }

@@ -154,6 +154,20 @@ __host__ __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k
     }
 }
 
+// SplitMix64 finaliser and the per-release stream seed (dpg.h
+// dpg_stream_seed; restated in oracle/dp_oracle.c).
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z ^= z >> 30;
+    z *= 0xBF58476D1CE4E5B9ull;
+    z ^= z >> 27;
+    z *= 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return z;
+}
+__host__ __device__ __forceinline__ uint64_t stream_seed(uint64_t seed, uint64_t nonce) {
+    return mix64(seed ^ mix64(nonce + 0x9E3779B97F4A7C15ull));
+}
+
 // Murmur3 finaliser (hash-table slots).
 __host__ __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
     h ^= h >> 16;

@@ -12,6 +12,7 @@ Device pipeline per call (include/dpg.h):
 """
 import ctypes
 import dataclasses
+import os
 from typing import Optional, Sequence
 
 import numpy as np
@@ -67,6 +68,16 @@ class DeviceAggregation:
         self._result: Optional[DeviceResult] = None
         self.last_partials = None
         self.noise_enabled = True
+        # Per-release nonce of every keyed random stream (include/dpg.h
+        # dpg_stream_seed).  None: drawn from os.urandom when the release is
+        # materialised, so two releases on one backend draw independent
+        # sampling, selection and noise, like the reference's fresh PyDP /
+        # numpy randomness per call (dp_computations.py:131-133, 151-152;
+        # pipeline_backend.py:540-544).  Tests inject it to reproduce a
+        # release; multi-GPU releases broadcast rank 0's.
+        self.nonce: Optional[int] = None
+        self.last_bound_fields: Optional[dict] = None
+        self.last_select_fields: Optional[dict] = None
 
     # ------------------------------------------------------------ public
     def __iter__(self):
@@ -104,10 +115,11 @@ class DeviceAggregation:
         return f
 
     def _select_fields(self, pk_offset: int, public_mask_local) -> dict:
+        nonce = self.nonce or 0
         if self.public_partitions is not None:
             return dict(strategy=0, table_len=0, keep_table=None, threshold=0.0,
                         noise_scale=0.0, pre_threshold=0, max_rows_per_privacy_id=1,
-                        pk_offset=pk_offset, public_mask=public_mask_local)
+                        pk_offset=pk_offset, public_mask=public_mask_local, nonce=nonce)
         spec = self.selection_spec
         sp = partition_selection.create_partition_selection_strategy(
             self.strategy, spec.eps, spec.delta, self.max_partitions_contributed,
@@ -117,17 +129,26 @@ class DeviceAggregation:
                  threshold=sp.threshold, noise_scale=sp.noise_scale,
                  pre_threshold=int(self.pre_threshold or 0),
                  max_rows_per_privacy_id=int(self.max_rows), pk_offset=pk_offset,
-                 public_mask=None)
+                 public_mask=None, nonce=nonce)
         if sp.table is not None:
             self._table = np.ascontiguousarray(np.asarray(sp.table, dtype=np.float64))
             f["table_len"] = len(self._table)
             f["keep_table"] = self._table.ctypes.data
         return f
 
+    def _release_nonce(self) -> int:
+        if self.nonce is None:
+            self.nonce = int.from_bytes(os.urandom(8), "little")
+        if self.backend.world_size > 1:
+            self.nonce = distributed.broadcast_u64(self.nonce, self.backend.process_group,
+                                                   self.backend.device)
+        return self.nonce
+
     def _run(self, gather: bool) -> DeviceResult:
         backend = self.backend
         ctx = backend.ctx
         dev = backend.device
+        nonce = self._release_nonce()
         need_values = self.plan is not None and self.plan.needs_values()
         enc = columnar.encode(self.col, self.extractors, dev, need_values,
                               self.public_partitions,
@@ -141,6 +162,12 @@ class DeviceAggregation:
                       scale=[0.0] * 4, mid=0.0, mean_const=0, msq_const=0,
                       mean_const_value=0.0, msq_const_value=0.0))
         P = enc.n_partitions
+        if backend.world_size > 1 and not enc.partitions_declared:
+            # every rank must use the same dense partition ids and P, or the
+            # exchange sums partials of different keys (or hangs)
+            raise ValueError(
+                "multi-GPU aggregation needs globally dense integer partition ids: "
+                "pass ColumnarData(..., n_partitions=P) with pk in [0, P) on every rank")
         with torch.cuda.device(dev):
             stream = torch.cuda.current_stream(dev)
             sptr = ctypes.c_void_p(stream.cuda_stream)
@@ -156,6 +183,9 @@ class DeviceAggregation:
             bound = _native.fill(_native.BoundParams, bfields)
             bound.pid_min, bound.pid_count = enc.pid_min, enc.pid_count
             bound.rec_id_offset = enc.rec_id_offset
+            bound.nonce = nonce
+            self.last_bound_fields = dict(bfields, pid_min=enc.pid_min, pid_count=enc.pid_count,
+                                          rec_id_offset=enc.rec_id_offset, nonce=nonce)
             if enc.public_mask is not None and self.drop_non_public:
                 bound.public_mask = enc.public_mask.data_ptr()
             partials = _native.Partials(P, rows.data_ptr(), count.data_ptr(),
@@ -176,12 +206,15 @@ class DeviceAggregation:
                 if public_mask_local is not None:
                     public_mask_local = distributed.slice_bitmap(
                         enc.public_mask, pk_offset, local_P)
+            # this rank's merged slice [pk_offset, pk_offset + local_P)
+            self.last_slice = (tensors, pk_offset, local_P)
             lp = _native.Partials(local_P, tensors["rows"].data_ptr(),
                                   tensors["count"].data_ptr(),
                                   *(tensors[k].data_ptr() if tensors[k] is not None else None
                                     for k in ("sum", "nsum", "nsq")))
             sfields = self._select_fields(
                 pk_offset, public_mask_local.data_ptr() if public_mask_local is not None else None)
+            self.last_select_fields = sfields
             sel = _native.fill(_native.SelectParams, sfields)
             nz = _native.fill(_native.NoiseParams, noise)
             n_out = noise["n_outputs"]

@@ -2,25 +2,34 @@
 
 Records are sharded by privacy id before they reach a rank (each privacy id
 lives on exactly one GPU), so contribution bounding is shard-local and the
-only exchange is the merge of the dense per-partition partials:
-`reduce_scatter` (sum) gives every rank an equal, contiguous slice of the
-partition space, the owner runs selection + noise for its slice, and the
-kept results are all-gathered.  Over RCCL/xGMI that is one reduce-scatter of
-8 B x P per accumulator array (P = 1e6: 8 MB each).  With gloo (CPU tests)
-the reduce-scatter is expressed as all_reduce + slice.
+only exchange is the merge of the dense per-partition partials: ONE
+`reduce_scatter` (sum) of all accumulator arrays packed together gives every
+rank an equal, contiguous slice of the partition space; the owner runs
+selection + noise for its slice, and the kept results are all-gathered.
 
-Every random draw is keyed by (seed, pid, pk) or (seed, pk) -- never by
-rank -- so the selected-partition set is identical for any world size.
+Over RCCL/xGMI that is one reduce-scatter of 8 B x P x (number of
+accumulator arrays) per release (P = 1e6, COUNT+SUM+PID: 24 MB).  The
+integer accumulators travel as float64, which is exact below 2^53 (a rank
+holds < 2^32 records, so no count comes near it).  With gloo (CPU tests,
+and several ranks sharing one GPU) the collectives are staged through host
+memory and the reduce-scatter is an all_reduce + slice.
+
+Every random draw is keyed by (stream seed, pid, pk) or (stream seed, pk)
+with global partition ids -- never by rank -- and the release nonce is
+broadcast from rank 0, so the selected-partition set is identical for any
+world size.
 """
 from typing import Dict, Optional, Tuple
 
 import torch
 import torch.distributed as dist
 
+_PACK_ORDER = ("rows", "count", "sum", "nsum", "nsq")
+
 
 def shard_of(pid: torch.Tensor, world_size: int) -> torch.Tensor:
     """Rank owning each privacy id (multiplicative hash, independent of the
-    fmix32 bits the kernels bucket by)."""
+    bits the kernels bucket by)."""
     h = (pid.to(torch.int64) * 0x9E3779B1) & 0xFFFFFFFF
     return ((h * world_size) >> 32).to(torch.int64)
 
@@ -31,31 +40,50 @@ def slice_bounds(P: int, world_size: int, rank: int) -> Tuple[int, int]:
     return lo, min(P, lo + chunk) - lo
 
 
+def _is_nccl(group) -> bool:
+    return dist.get_backend(group) == "nccl"
+
+
+def broadcast_u64(x: int, group, device) -> int:
+    """Rank 0's 64-bit value on every rank (the release nonce)."""
+    signed = x - (1 << 64) if x >= (1 << 63) else x
+    dev = device if _is_nccl(group) else torch.device("cpu")
+    t = torch.tensor([signed], dtype=torch.int64, device=dev)
+    dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None else 0,
+                   group=group)
+    return int(t.item()) & ((1 << 64) - 1)
+
+
 def reduce_scatter_partials(tensors: Dict[str, Optional[torch.Tensor]], P: int, group
                             ) -> Tuple[Dict[str, Optional[torch.Tensor]], int, int]:
+    """Sums the dense partials over ranks and returns this rank's slice
+    [lo, lo + n) of every array, with one collective for all of them."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     chunk = (P + world - 1) // world
     padded = chunk * world
     lo, n_local = slice_bounds(P, world, rank)
-    out: Dict[str, Optional[torch.Tensor]] = {}
-    use_rs = dist.get_backend(group) == "nccl"
-    for name, t in tensors.items():
-        if t is None:
-            out[name] = None
-            continue
-        full = t
-        if padded != P:
-            full = torch.zeros(padded, dtype=t.dtype, device=t.device)
-            full[:P] = t
-        if use_rs:
-            part = torch.empty(chunk, dtype=t.dtype, device=t.device)
-            dist.reduce_scatter_tensor(part, full, op=dist.ReduceOp.SUM, group=group)
-        else:
-            full = full.clone()
-            dist.all_reduce(full, op=dist.ReduceOp.SUM, group=group)
-            part = full[rank * chunk:(rank + 1) * chunk]
-        out[name] = part[:n_local].contiguous()
+    names = [k for k in _PACK_ORDER if tensors.get(k) is not None]
+    like = tensors[names[0]]
+    dev = like.device
+    # layout [world][array][chunk]: rank r's reduce-scatter block is the
+    # contiguous [array][chunk] slab of its partition slice
+    pack = torch.zeros((len(names), padded), dtype=torch.float64, device=dev)
+    for j, k in enumerate(names):
+        pack[j, :P] = tensors[k].to(torch.float64)
+    pack = pack.view(len(names), world, chunk).transpose(0, 1).contiguous()
+    if _is_nccl(group):
+        part = torch.empty((len(names), chunk), dtype=torch.float64, device=dev)
+        dist.reduce_scatter_tensor(part, pack, op=dist.ReduceOp.SUM, group=group)
+    else:
+        host = pack.cpu()
+        dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
+        part = host[rank].to(dev)
+    out: Dict[str, Optional[torch.Tensor]] = {k: None for k in _PACK_ORDER}
+    for j, k in enumerate(names):
+        col = part[j, :n_local]
+        out[k] = (col.round().to(torch.int64) if tensors[k].dtype == torch.int64
+                  else col).contiguous()
     return out, lo, n_local
 
 
@@ -70,24 +98,24 @@ def slice_bitmap(mask: torch.Tensor, lo: int, n: int) -> torch.Tensor:
 
 
 def all_gather_results(ids: torch.Tensor, vals: torch.Tensor, group):
+    """Concatenates every rank's kept (ids, values) in rank order: one size
+    exchange, then one all_gather of ids and values packed as float64 rows
+    (ids < 2^32 are exact)."""
     world = dist.get_world_size(group)
-    n = torch.tensor([ids.numel()], dtype=torch.int64, device=ids.device)
+    nccl = _is_nccl(group)
+    dev = ids.device
+    cdev = dev if nccl else torch.device("cpu")
+    n = torch.tensor([ids.numel()], dtype=torch.int64, device=cdev)
     sizes = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(sizes, n, group=group)
     sizes = [int(s.item()) for s in sizes]
     m = max(sizes) if sizes else 0
     cols = vals.shape[1] if vals.dim() == 2 else 0
-    pid = torch.full((m,), -1, dtype=torch.int64, device=ids.device)
-    pid[:ids.numel()] = ids
-    pv = torch.zeros((m, cols), dtype=vals.dtype, device=vals.device)
+    buf = torch.zeros((m, 1 + cols), dtype=torch.float64, device=cdev)
+    buf[:ids.numel(), 0] = ids.to(torch.float64).to(cdev)
     if cols:
-        pv[:ids.numel()] = vals
-    g_ids = [torch.empty_like(pid) for _ in range(world)]
-    dist.all_gather(g_ids, pid, group=group)
-    g_vals = [torch.empty_like(pv) for _ in range(world)]
-    if cols:
-        dist.all_gather(g_vals, pv, group=group)
-    ids_all = torch.cat([g[:s] for g, s in zip(g_ids, sizes)])
-    vals_all = (torch.cat([g[:s] for g, s in zip(g_vals, sizes)]) if cols else
-                torch.empty((ids_all.numel(), 0), dtype=vals.dtype, device=vals.device))
-    return ids_all, vals_all
+        buf[:ids.numel(), 1:] = vals.to(cdev)
+    got = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(got, buf, group=group)
+    rows = torch.cat([g[:s] for g, s in zip(got, sizes)]).to(dev)
+    return rows[:, 0].round().to(torch.int64), rows[:, 1:].to(vals.dtype).contiguous()

@@ -44,7 +44,11 @@ def _gaussian_delta(sigma: float, eps: float, l2: float) -> float:
     mechanism, Balle & Wang 2018)."""
     a = l2 / (2.0 * sigma)
     b = eps * sigma / l2
-    return _std_normal_cdf(a - b) - math.exp(eps) * _std_normal_cdf(-a - b)
+    if eps < 700.0:
+        return _std_normal_cdf(a - b) - math.exp(eps) * _std_normal_cdf(-a - b)
+    # e^eps overflows a double: evaluate e^eps * Phi(-a-b) in the log domain
+    from scipy.special import log_ndtr
+    return _std_normal_cdf(a - b) - math.exp(min(700.0, eps + float(log_ndtr(-a - b))))
 
 
 def compute_sigma(eps: float, delta: float, l2_sensitivity: float) -> float:

@@ -1,0 +1,147 @@
+"""GPU parity at BASELINE.json shapes (reduced record counts so the oracle
+finishes in seconds): the config-2 generator at 1e7 records, and the config-4
+shape (Pareto(1.2) records per privacy id, mpc = 50, mcpp = 4, P = 1e8,
+MEAN+VARIANCE with Gaussian noise) with public and with private partitions.
+The config-4 data holds privacy ids with tens of thousands of records, so
+their buckets take the global-memory kernel (k_bound_big) with 32-byte
+MEAN/VARIANCE items."""
+import numpy as np
+import pytest
+import torch
+
+import bench
+import pipelinedp_amd as pdp
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+SEED = 0xC0F16
+
+
+def _run(pid, pk, val, params, P, public=None, noise=False, nonce=1234, pid_range=None):
+    backend = pdp.MI355XBackend(device=0, seed=SEED)
+    acc = pdp.NaiveBudgetAccountant(1.0, 1e-6)
+    cols = pdp.ColumnarData(pid=torch.from_numpy(pid).cuda(), pk=torch.from_numpy(pk).cuda(),
+                            value=torch.from_numpy(val).cuda(), n_partitions=P,
+                            privacy_id_range=pid_range)
+    res = pdp.DPEngine(acc, backend).aggregate(cols, params, pdp.DataExtractors("pid", "pk", "value"),
+                                               public_partitions=public)
+    acc.compute_budgets()
+    res.noise_enabled = noise
+    res.nonce = nonce
+    out = res.materialize()
+    got = {k: v.cpu().numpy() for k, v in res.last_partials.items() if v is not None}
+    return res, out, got
+
+
+def _assert_partials(got, ref, keys=("sum",)):
+    assert np.array_equal(got["rows"], ref["rows"])
+    assert np.array_equal(got["count"], ref["count"])
+    for k in keys:
+        assert np.allclose(got[k], ref[k], rtol=1e-9, atol=1e-9), k
+
+
+# ------------------------------------------------------------------ config 2
+N2, U2, P2 = 10_000_000, 100_000, 1_000_000
+
+
+@pytest.fixture(scope="module")
+def config2_data():
+    pid, pk, val = bench.host_sample(N2, U2, P2, 2024)
+    return pid.astype(np.int64), pk.astype(np.int64), val
+
+
+def _c2_params(mpc, mcpp):
+    return pdp.AggregateParams(
+        metrics=[pdp.Metrics.COUNT, pdp.Metrics.SUM, pdp.Metrics.PRIVACY_ID_COUNT],
+        noise_kind=pdp.NoiseKind.LAPLACE, max_partitions_contributed=mpc,
+        max_contributions_per_partition=mcpp, min_value=0.0, max_value=10.0)
+
+
+def test_config2_nonbinding_bounds_equal_exact_groupby(built, config2_data):
+    """SURVEY 8(d) parity variant: 1e7 records of the config-2 generator with
+    bounds that never trigger; the partials are the exact group-by of the
+    input (numpy, independent of the oracle): counts and privacy-id counts
+    bit-exact, sums within 1e-9 relative."""
+    pid, pk, val = config2_data
+    _, _, got = _run(pid, pk, val, _c2_params(10**6, 10**6), P2, pid_range=(0, U2))
+    count = np.bincount(pk, minlength=P2)
+    s = np.bincount(pk, weights=np.clip(val, 0.0, 10.0), minlength=P2)
+    pairs = np.unique(pid * P2 + pk)
+    rows = np.bincount(pairs % P2, minlength=P2)
+    assert np.array_equal(got["count"], count)
+    assert np.array_equal(got["rows"], rows)
+    assert np.allclose(got["sum"], s, rtol=1e-9, atol=1e-9)
+
+
+def test_config2_bounding_triggered_matches_oracle(built, config2_data):
+    """mpc = 8, mcpp = 2 (the bench's bounds): partials equal the oracle's,
+    then selection + Laplace noise equal the oracle's release."""
+    pid, pk, val = config2_data
+    res, out, got = _run(pid, pk, val, _c2_params(8, 2), P2, noise=True)
+    ref = oracle.bound_aggregate(pid, pk, val, res.last_bound_fields, SEED)
+    _assert_partials(got, ref)
+    assert got["rows"].sum() <= 8 * U2
+    keep, o = oracle.select_and_noise(ref, res.last_select_fields, res.plan.noise_fields(True),
+                                      SEED, keep_table=res._table)
+    ids = np.nonzero(keep)[0]
+    gid = out.partition_ids.cpu().numpy()
+    assert np.array_equal(np.sort(gid), ids)
+    assert np.allclose(out.values.cpu().numpy()[np.argsort(gid)], o[ids], rtol=1e-12, atol=1e-6)
+
+
+# ------------------------------------------------------------------ config 4
+N4, U4, P4 = 20_000_000, 100_000, 100_000_000
+
+
+@pytest.fixture(scope="module")
+def config4_data():
+    pid, pk, val = bench.host_sample(N4, U4, P4, 4242, pareto=(1.2, 1000.0))
+    pid, pk = pid.astype(np.int64), pk.astype(np.int64)
+    # heavy privacy ids: far beyond one LDS chunk (1024 records), so the
+    # global-memory bounding kernel runs
+    assert np.bincount(pid).max() > 8192
+    return pid, pk, val
+
+
+def _c4_params():
+    return pdp.AggregateParams(
+        metrics=[pdp.Metrics.MEAN, pdp.Metrics.VARIANCE], noise_kind=pdp.NoiseKind.GAUSSIAN,
+        max_partitions_contributed=50, max_contributions_per_partition=4,
+        min_value=0.0, max_value=10.0)
+
+
+def test_config4_public_partitions_match_oracle(built, config4_data):
+    """public_partitions = range(1e8): non-public drop + empty partitions,
+    MEAN/VARIANCE moments through every bounding kernel (Item32), noise-free
+    outputs equal the oracle's for all 1e8 partitions."""
+    pid, pk, val = config4_data
+    res, out, got = _run(pid, pk, val, _c4_params(), P4, public=range(P4))
+    mask = np.full((P4 + 7) // 8, 0xFF, np.uint8)
+    ref = oracle.bound_aggregate(pid, pk, val, res.last_bound_fields, SEED, public_mask=mask)
+    _assert_partials(got, ref, keys=("nsum", "nsq"))
+    assert out.partition_ids.numel() == P4
+    keep, o = oracle.select_and_noise(ref, res.last_select_fields, res.plan.noise_fields(False),
+                                      SEED, public_mask=mask)
+    assert keep.all()
+    gid = out.partition_ids.cpu().numpy()
+    assert np.array_equal(gid, np.arange(P4))
+    assert np.allclose(out.values.cpu().numpy(), o, rtol=1e-9, atol=1e-9, equal_nan=True)
+
+
+def test_config4_private_selection_gaussian_matches_oracle(built, config4_data):
+    """Private selection (truncated geometric, l0 = 50) + Gaussian noise on
+    the 3-way-split VARIANCE mechanism: keep set and noised mean/variance
+    equal the oracle's release."""
+    pid, pk, val = config4_data
+    res, out, got = _run(pid, pk, val, _c4_params(), P4, noise=True, nonce=99)
+    ref = oracle.bound_aggregate(pid, pk, val, res.last_bound_fields, SEED)
+    _assert_partials(got, ref, keys=("nsum", "nsq"))
+    assert got["rows"].max() > 0
+    keep, o = oracle.select_and_noise(ref, res.last_select_fields, res.plan.noise_fields(True),
+                                      SEED, keep_table=res._table)
+    ids = np.nonzero(keep)[0]
+    gid = out.partition_ids.cpu().numpy()
+    assert np.array_equal(np.sort(gid), ids)
+    assert len(ids) > 100
+    assert np.allclose(out.values.cpu().numpy()[np.argsort(gid)], o[ids], rtol=1e-9, atol=1e-6)

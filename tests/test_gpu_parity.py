@@ -15,7 +15,7 @@ SEED = 0x5EED
 
 
 def run_engine(pid, pk, value, params, public=None, seed=SEED, noise=False,
-               n_partitions=None, eps=1.0, delta=1e-6):
+               n_partitions=None, eps=1.0, delta=1e-6, nonce=None):
     backend = pdp.MI355XBackend(device=0, seed=seed)
     acc = pdp.NaiveBudgetAccountant(eps, delta)
     eng = pdp.DPEngine(acc, backend)
@@ -26,6 +26,8 @@ def run_engine(pid, pk, value, params, public=None, seed=SEED, noise=False,
                         public_partitions=public)
     acc.compute_budgets()
     res.noise_enabled = noise
+    if nonce is not None:
+        res.nonce = nonce
     out = res.materialize()
     return res, out
 
@@ -89,7 +91,7 @@ def test_gpu_bounding_matches_oracle_exactly(built, name, kw, dup):
     res, _ = run_engine(pid, pk, val, params, public=list(range(P)), n_partitions=P)
     plan = res.plan
     ref = oracle.bound_aggregate(pid, pk, val if plan.needs_values() else None,
-                                 plan.bound_fields(P), SEED, public_mask=oracle.bitmap(range(P), P))
+                                 res.last_bound_fields, SEED, public_mask=oracle.bitmap(range(P), P))
     got = {k: (v.cpu().numpy() if v is not None else None) for k, v in res.last_partials.items()}
     assert np.array_equal(got["rows"], ref["rows"])
     assert np.array_equal(got["count"], ref["count"])
@@ -109,8 +111,8 @@ def test_gpu_selection_and_noise_match_oracle(built):
         min_value=0.0, max_value=10.0)
     res, out = run_engine(pid, pk, val, params, noise=True, n_partitions=P)
     plan = res.plan
-    ref = oracle.bound_aggregate(pid, pk, val, plan.bound_fields(P), SEED)
-    sel = res._select_fields(0, None)
+    ref = oracle.bound_aggregate(pid, pk, val, res.last_bound_fields, SEED)
+    sel = res.last_select_fields
     keep, o = oracle.select_and_noise(ref, sel, plan.noise_fields(True), SEED,
                                       keep_table=res._table)
     ids = np.nonzero(keep)[0]
@@ -140,7 +142,7 @@ def test_gpu_partition_levels_and_fallback(built, target, cap):
     acc.compute_budgets()
     res.noise_enabled = False
     res.materialize()
-    ref = oracle.bound_aggregate(pid, pk, val, res.plan.bound_fields(P), SEED,
+    ref = oracle.bound_aggregate(pid, pk, val, res.last_bound_fields, SEED,
                                  public_mask=oracle.bitmap(range(P), P))
     got = {k: v.cpu().numpy() for k, v in res.last_partials.items() if v is not None}
     assert np.array_equal(got["rows"], ref["rows"])
@@ -166,17 +168,27 @@ def test_gpu_key_range_error(built):
         run_engine(np.array([1, 2]), np.array([0, 10]), None, params, n_partitions=5)
 
 
-def test_gpu_determinism_same_seed(built):
+def test_gpu_determinism_same_seed_and_nonce(built):
+    """A release is a pure function of (seed, nonce): the same pair
+    reproduces it bit for bit; another nonce (the default: fresh per
+    release) draws independent selection and noise."""
     P = 2000
     pid, pk, val = _dataset(3, 200_000, 5_000, P)
     params = pdp.AggregateParams(metrics=[pdp.Metrics.COUNT, pdp.Metrics.SUM,
                                           pdp.Metrics.PRIVACY_ID_COUNT],
                                  max_partitions_contributed=2, max_contributions_per_partition=1,
                                  min_value=0.0, max_value=10.0)
-    a = run_engine(pid, pk, val, params, noise=True, n_partitions=P)[1]
-    b = run_engine(pid, pk, val, params, noise=True, n_partitions=P)[1]
+    a = run_engine(pid, pk, val, params, noise=True, n_partitions=P, nonce=42)[1]
+    b = run_engine(pid, pk, val, params, noise=True, n_partitions=P, nonce=42)[1]
     assert np.array_equal(a.partition_ids.cpu().numpy(), b.partition_ids.cpu().numpy())
-    assert np.allclose(a.values.cpu().numpy(), b.values.cpu().numpy(), rtol=1e-12, atol=1e-9)
+    assert np.allclose(a.values.cpu().numpy(), b.values.cpu().numpy(), rtol=1e-12, atol=1e-6)
+    c = run_engine(pid, pk, val, params, noise=True, n_partitions=P, nonce=43)[1]
+    ka, kc = a.partition_ids.cpu().numpy(), c.partition_ids.cpu().numpy()
+    common = np.intersect1d(ka, kc)
+    va = a.values.cpu().numpy()[np.searchsorted(ka, common)]
+    vc = c.values.cpu().numpy()[np.searchsorted(kc, common)]
+    assert not np.array_equal(ka, kc) or not np.array_equal(va, vc)
+    assert (va != vc).all(axis=1).mean() > 0.9
 
 
 _NO_NOISE = dict(noise_kind=0, family=0, slot_mask=0, n_outputs=0, out_src=[0] * 8,
@@ -203,10 +215,10 @@ def test_gpu_select_partitions_matches_oracle(built, strategy):
     res = eng.select_partitions(cols, params, pdp.DataExtractors("pid", "pk"))
     acc.compute_budgets()
     out = res.materialize()
-    ref = oracle.bound_aggregate(pid, pk, None, res._bound_fields(P), SEED)
+    ref = oracle.bound_aggregate(pid, pk, None, res.last_bound_fields, SEED)
     got_rows = res.last_partials["rows"].cpu().numpy()
     assert np.array_equal(got_rows, ref["rows"])
-    keep, _ = oracle.select_and_noise(ref, res._select_fields(0, None), _NO_NOISE, SEED,
+    keep, _ = oracle.select_and_noise(ref, res.last_select_fields, _NO_NOISE, SEED,
                                       keep_table=getattr(res, "_table", None))
     want = np.nonzero(keep)[0]
     assert 0 < len(want) < P
@@ -232,7 +244,7 @@ def test_gpu_heavy_privacy_ids(built):
         max_partitions_contributed=40, max_contributions_per_partition=3,
         min_value=0.0, max_value=10.0)
     res, _ = run_engine(pid, pk, val, params, public=list(range(P)), n_partitions=P)
-    ref = oracle.bound_aggregate(pid, pk, val, res.plan.bound_fields(P), SEED,
+    ref = oracle.bound_aggregate(pid, pk, val, res.last_bound_fields, SEED,
                                  public_mask=oracle.bitmap(range(P), P))
     got = {k: v.cpu().numpy() for k, v in res.last_partials.items() if v is not None}
     assert np.array_equal(got["rows"], ref["rows"])
@@ -256,7 +268,7 @@ def test_gpu_large_partition_space(built, P):
                                  max_partitions_contributed=4, max_contributions_per_partition=2,
                                  min_value=0.0, max_value=10.0)
     res, _ = run_engine(pid, pk, val, params, n_partitions=P)
-    ref = oracle.bound_aggregate(pid, pk, val, res.plan.bound_fields(P), SEED)
+    ref = oracle.bound_aggregate(pid, pk, val, res.last_bound_fields, SEED)
     got = {k: v.cpu().numpy() for k, v in res.last_partials.items() if v is not None}
     assert np.array_equal(got["rows"], ref["rows"])
     assert np.array_equal(got["count"], ref["count"])
@@ -280,7 +292,7 @@ def test_gpu_wide_records(built):
                                  max_partitions_contributed=3, max_contributions_per_partition=2,
                                  min_value=0.0, max_value=10.0)
     res, _ = run_engine(pid, pk, val, params, n_partitions=P)
-    ref = oracle.bound_aggregate(pid, pk, val, res.plan.bound_fields(P), SEED)
+    ref = oracle.bound_aggregate(pid, pk, val, res.last_bound_fields, SEED)
     got = {k: v.cpu().numpy() for k, v in res.last_partials.items() if v is not None}
     assert np.array_equal(got["rows"], ref["rows"])
     assert np.array_equal(got["count"], ref["count"])

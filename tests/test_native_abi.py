@@ -48,6 +48,19 @@ def test_struct_layouts_match_c(tmp_path):
     assert got == want
 
 
+def test_stream_seed_matches_oracle(built):
+    """dpg_stream_seed (pure host function) equals the oracle's restatement,
+    and distinct nonces give distinct stream seeds."""
+    from oracle import oracle
+    seeds = set()
+    for seed in (0, 1, 0x5EED, 2**64 - 1):
+        for nonce in (0, 1, 2, 0xDEADBEEF, 2**63):
+            s = _native.stream_seed(seed, nonce)
+            assert s == oracle.stream_seed(seed, nonce)
+            seeds.add(s)
+    assert len(seeds) == 20
+
+
 def test_no_cpu_fallback_without_gpu():
     import torch
     import pipelinedp_amd as pdp
