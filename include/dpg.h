@@ -21,6 +21,14 @@
  *        dp_computations.py:120-184, 307-366, 541-576; PyDP add_noise).
  *   dpg_compact_kept     <- the LocalBackend `filter` materialisation
  *        (pipeline_backend.py:514-515) of the selected partitions.
+ *   dpg_preaggregate     <- utility analysis' per-(privacy id, partition)
+ *        pre-aggregation: analysis/contribution_bounders.py:37-77
+ *        (AnalysisContributionBounder) and analysis/pre_aggregation.py:19-61.
+ *   dpg_utility_analysis <- the per-partition utility combiners of every
+ *        configuration of a sweep: analysis/per_partition_combiners.py:195-356
+ *        (PartitionSelection / Sum / Count / PrivacyIdCount / RawStatistics)
+ *        with analysis/poisson_binomial.py:39-83, driven by
+ *        analysis/utility_analysis_engine.py:98-143.
  */
 #ifndef DPG_H_
 #define DPG_H_
@@ -167,6 +175,45 @@ typedef struct dpg_noise_params {
     double msq_const_value;
 } dpg_noise_params;
 
+/* One (privacy id, partition) pair of the utility-analysis pre-aggregate
+ * (32 bytes): the pair's record count and value sum, the number of
+ * partitions its privacy id contributes to and the privacy id's records. */
+typedef struct dpg_pair_entry {
+    uint32_t pk;
+    uint32_t count;
+    double sum;
+    uint32_t n_partitions;
+    uint32_t n_contributions;
+    uint32_t reserved[2];
+} dpg_pair_entry;
+
+/* One row of a MultiParameterConfiguration (analysis/data_structures.py
+ * :24-103) with the budget of its mechanisms resolved. */
+typedef struct dpg_ua_config {
+    int64_t max_partitions_contributed;      /* l0                          */
+    int64_t max_contributions_per_partition; /* linf of COUNT               */
+    double min_sum_per_partition;            /* SUM clipping                */
+    double max_sum_per_partition;
+    int32_t selection_strategy;  /* DPG_SELECT_* (private partitions)      */
+    int32_t reserved;
+    int64_t pre_threshold;       /* 0 = none                               */
+    const double *keep_table;    /* host: truncated geometric pi(n)        */
+    int64_t table_len;
+    double threshold;            /* Laplace / Gaussian thresholding        */
+    double noise_scale;
+} dpg_ua_config;
+
+typedef struct dpg_ua_params {
+    int32_t n_configs;           /* 1..64                                   */
+    uint32_t metric_mask;        /* DPG_M_SUM | DPG_M_COUNT | DPG_M_PRIVACY_ID_COUNT */
+    int32_t public_partitions;   /* 1: public partitions (no selection)    */
+    int32_t reserved;
+    const dpg_ua_config *configs;/* host [n_configs]                       */
+    const uint8_t *sample_mask;  /* device bitmap of the partitions kept by
+                                    partitions_sampling_prob, or NULL       */
+    const uint8_t *public_mask;  /* device bitmap of public partitions     */
+} dpg_ua_params;
+
 typedef struct dpg_ctx dpg_ctx;
 
 /* Context: device ordinal and the 64-bit seed of every keyed random stream.
@@ -217,6 +264,35 @@ int dpg_compact_kept(dpg_ctx *ctx, const uint8_t *keep, const double *out,
                      int64_t n_partitions, int32_t n_outputs,
                      int64_t *kept_ids, double *kept_out, int64_t *n_kept,
                      void *stream);
+
+/* Utility-analysis pre-aggregate: no contribution bounding; one entry per
+ * distinct (privacy id, partition) pair, sorted by partition key, into
+ * pairs[0, *n_pairs) (device, `capacity` entries; n always suffices), and
+ * partition_start (device int64[P + 1]): the pairs of partition k are
+ * [partition_start[k], partition_start[k + 1]).  Of *p only n_partitions,
+ * public_mask (pairs of other partitions are dropped first), pid_min,
+ * pid_count and rec_id_offset are used.  value may be NULL (sums 0).
+ * *n_pairs (host) receives the pair count (synchronises the stream); if it
+ * exceeds capacity the call fails with DPG_ERR_INVALID_ARG. */
+int dpg_preaggregate(dpg_ctx *ctx, const int64_t *pid, const int64_t *pk, const double *value,
+                     int64_t n, const dpg_bound_params *p, dpg_pair_entry *pairs,
+                     int64_t capacity, int64_t *partition_start, int64_t *n_pairs,
+                     void *stream);
+
+/* Per-partition utility analysis of up to 64 configurations in one pass
+ * over the sorted pre-aggregate.  Device outputs:
+ *   raw    double[P][2]: privacy id count, count (RawStatistics)
+ *   errors double[P][M][5][C], M = metrics present in the order SUM, COUNT,
+ *          PRIVACY_ID_COUNT; the 5 fields are sum, clipping_to_min_error,
+ *          clipping_to_max_error, expected_l0_bounding_error and the l0
+ *          bounding variance (SumMetrics before the noise std is attached)
+ *   keep   double[P][C]: partition_selection_probability_to_keep (NULL for
+ *          public partitions).
+ * Partitions outside sample_mask or without pairs (and not public) stay 0. */
+int dpg_utility_analysis(dpg_ctx *ctx, const dpg_pair_entry *pairs,
+                         const int64_t *partition_start, int64_t n_partitions,
+                         const dpg_ua_params *params, double *raw, double *errors, double *keep,
+                         void *stream);
 
 /* Timing/profiling aid: per-stage device time (ms) of the last
  * dpg_bound_aggregate call, measured with HIP events on its stream.

@@ -17,7 +17,8 @@ ERRORS = {1: "invalid argument", 2: "key out of range", 3: "HIP error",
 EXPORTED = ("dpg_ctx_create", "dpg_ctx_destroy", "dpg_last_error", "dpg_set_seed",
             "dpg_set_tuning",
             "dpg_bound_aggregate", "dpg_select_and_noise", "dpg_compact_kept",
-            "dpg_last_stage_times", "dpg_stream_seed")
+            "dpg_last_stage_times", "dpg_stream_seed", "dpg_preaggregate",
+            "dpg_utility_analysis")
 
 
 class BoundParams(ctypes.Structure):
@@ -56,6 +57,31 @@ class NoiseParams(ctypes.Structure):
                 ("mid", ctypes.c_double), ("mean_const", ctypes.c_int32),
                 ("msq_const", ctypes.c_int32), ("mean_const_value", ctypes.c_double),
                 ("msq_const_value", ctypes.c_double)]
+
+
+class PairEntry(ctypes.Structure):
+    """dpg_pair_entry: one (privacy id, partition) pair of the pre-aggregate."""
+    _fields_ = [("pk", ctypes.c_uint32), ("count", ctypes.c_uint32), ("sum", ctypes.c_double),
+                ("n_partitions", ctypes.c_uint32), ("n_contributions", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32 * 2)]
+
+
+class UaConfig(ctypes.Structure):
+    _fields_ = [("max_partitions_contributed", ctypes.c_int64),
+                ("max_contributions_per_partition", ctypes.c_int64),
+                ("min_sum_per_partition", ctypes.c_double),
+                ("max_sum_per_partition", ctypes.c_double),
+                ("selection_strategy", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("pre_threshold", ctypes.c_int64), ("keep_table", ctypes.c_void_p),
+                ("table_len", ctypes.c_int64), ("threshold", ctypes.c_double),
+                ("noise_scale", ctypes.c_double)]
+
+
+class UaParams(ctypes.Structure):
+    _fields_ = [("n_configs", ctypes.c_int32), ("metric_mask", ctypes.c_uint32),
+                ("public_partitions", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("configs", ctypes.c_void_p), ("sample_mask", ctypes.c_void_p),
+                ("public_mask", ctypes.c_void_p)]
 
 
 def fill(struct_type, fields: dict):
@@ -122,6 +148,12 @@ def load():
         lib.dpg_compact_kept.argtypes = [vp, vp, vp, i64, i32, vp, vp,
                                          ctypes.POINTER(ctypes.c_int64), vp]
         lib.dpg_compact_kept.restype = ctypes.c_int
+        lib.dpg_preaggregate.argtypes = [vp, vp, vp, vp, i64, ctypes.POINTER(BoundParams), vp,
+                                         i64, vp, ctypes.POINTER(ctypes.c_int64), vp]
+        lib.dpg_preaggregate.restype = ctypes.c_int
+        lib.dpg_utility_analysis.argtypes = [vp, vp, vp, i64, ctypes.POINTER(UaParams), vp, vp,
+                                             vp, vp]
+        lib.dpg_utility_analysis.restype = ctypes.c_int
         lib.dpg_last_stage_times.argtypes = [vp, ctypes.c_char_p, ctypes.c_size_t,
                                              ctypes.POINTER(ctypes.c_double), i32,
                                              ctypes.POINTER(ctypes.c_int32)]
@@ -194,6 +226,22 @@ class Context:
                                        ids_ptr, kept_out_ptr, ctypes.byref(n), stream)
         self.check(st, "dpg_compact_kept")
         return n.value
+
+    def preaggregate(self, pid_ptr, pk_ptr, value_ptr, n, bound: BoundParams, pairs_ptr,
+                     capacity, starts_ptr, stream) -> int:
+        n_pairs = ctypes.c_int64(0)
+        st = self.lib.dpg_preaggregate(self.handle, pid_ptr, pk_ptr, value_ptr, n,
+                                       ctypes.byref(bound), pairs_ptr, capacity, starts_ptr,
+                                       ctypes.byref(n_pairs), stream)
+        self.check(st, "dpg_preaggregate")
+        return n_pairs.value
+
+    def utility_analysis(self, pairs_ptr, starts_ptr, n_partitions, params: UaParams, raw_ptr,
+                         err_ptr, keep_ptr, stream):
+        st = self.lib.dpg_utility_analysis(self.handle, pairs_ptr, starts_ptr, n_partitions,
+                                           ctypes.byref(params), raw_ptr, err_ptr, keep_ptr,
+                                           stream)
+        self.check(st, "dpg_utility_analysis")
 
     def stage_times(self):
         names = ctypes.create_string_buffer(1024)

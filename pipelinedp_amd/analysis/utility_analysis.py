@@ -1,0 +1,485 @@
+"""Utility analysis of many contribution-bound configurations in one device
+pass (API mirror of analysis/utility_analysis.py:42-144 and
+analysis/utility_analysis_engine.py:29-218).
+
+The reference subclasses DPEngine and swaps graph nodes: the contribution
+bounder becomes a per-(privacy id, partition) pre-aggregation
+(analysis/contribution_bounders.py:37-77), the compound combiner holds one
+set of per-partition utility combiners per configuration
+(utility_analysis_engine.py:98-143) and private selection becomes a
+keep-probability computation.  On MI355X that is two C-ABI calls:
+
+  dpg_preaggregate      all (pid, pk) pairs with (count, sum, n_partitions,
+                        n_contributions), sorted by partition key
+  dpg_utility_analysis  every configuration's per-partition combiners in one
+                        pass over the pairs (lane = configuration)
+
+followed by the cross-partition combine (cross_partition_combiners.py
+:264-343, utility_analysis.py:196-251), a weighted sum over partitions per
+(configuration, partition-size bucket) done with device tensor reductions.
+The budget is requested and resolved exactly as the reference does it.
+"""
+import bisect
+import ctypes
+import dataclasses
+import hashlib
+import math
+from typing import Any, Dict, Iterable, List, Optional, Sequence, Tuple, Union
+
+import numpy as np
+import torch
+
+from pipelinedp_amd import _native
+from pipelinedp_amd import aggregate_params as agg
+from pipelinedp_amd import budget_accounting
+from pipelinedp_amd import columnar
+from pipelinedp_amd import data_extractors as dex
+from pipelinedp_amd import dp_computations as dpc
+from pipelinedp_amd import partition_selection
+from pipelinedp_amd import pipeline_backend
+from pipelinedp_amd.analysis import data_structures
+from pipelinedp_amd.analysis import metrics
+
+M_COUNT, M_SUM, M_PID = 1, 2, 4
+# per-partition metric blocks of dpg_utility_analysis, in this order
+_BLOCKS = ((agg.Metrics.SUM, M_SUM), (agg.Metrics.COUNT, M_COUNT),
+           (agg.Metrics.PRIVACY_ID_COUNT, M_PID))
+
+
+def _generate_bucket_bounds():
+    result = [0, 1]
+    for i in range(1, 10):
+        result += [10**i, 2 * 10**i, 5 * 10**i]
+    return tuple(result)
+
+
+# partition-size histogram bounds (utility_analysis.py:29-39)
+BUCKET_BOUNDS = _generate_bucket_bounds()
+
+
+def _get_lower_bound(n) -> int:
+    if n < 0:
+        return 0
+    return BUCKET_BOUNDS[bisect.bisect_right(BUCKET_BOUNDS, n) - 1]
+
+
+def _get_upper_bound(n) -> int:
+    if n < 0:
+        return 0
+    i = bisect.bisect_right(BUCKET_BOUNDS, n)
+    return BUCKET_BOUNDS[i] if i < len(BUCKET_BOUNDS) else -1
+
+
+def _check_options(options: data_structures.UtilityAnalysisOptions, extractors):
+    """utility_analysis_engine.py:187-218."""
+    if options.pre_aggregated_data:
+        if not isinstance(extractors, dex.PreAggregateExtractors):
+            raise ValueError(
+                "options.pre_aggregated_data is set to true but PreAggregateExtractors aren't "
+                "provided. PreAggregateExtractors should be specified for pre-aggregated data.")
+    elif not isinstance(extractors, dex.DataExtractors):
+        raise ValueError("pipeline_dp.DataExtractors should be specified for raw data.")
+    params = options.aggregate_params
+    if params.custom_combiners is not None:
+        raise NotImplementedError("custom combiners are not supported")
+    allowed = {agg.Metrics.COUNT, agg.Metrics.SUM, agg.Metrics.PRIVACY_ID_COUNT}
+    if not set(params.metrics).issubset(allowed):
+        raise NotImplementedError(
+            f"unsupported metric in metrics={list(set(params.metrics) - allowed)}")
+    if params.contribution_bounds_already_enforced:
+        raise NotImplementedError("utility analysis when contribution bounds are already "
+                                  "enforced is not supported")
+    if options.n_configurations > 64:
+        raise NotImplementedError("at most 64 configurations per sweep (one per wave lane)")
+
+
+def _noise_std(noise_kind, eps: float, delta: float, l0: float, linf: float) -> float:
+    """dp_computations.py:369-388 (compute_dp_count_noise_std)."""
+    if noise_kind == agg.NoiseKind.LAPLACE:
+        return (l0 * linf / eps) * math.sqrt(2)
+    return dpc.compute_sigma(eps, delta, math.sqrt(l0) * linf)
+
+
+def _sample_bound(prob: float) -> int:
+    return int(round(2**64 * prob))
+
+
+def _keep_by_hash(key, bound: int) -> bool:
+    """sampling_utils.ValueSampler.keep (sampling_utils.py:32-51)."""
+    h = int(hashlib.sha1(repr(key).encode()).hexdigest()[:16], 16)
+    return h < bound
+
+
+@dataclasses.dataclass
+class _Config:
+    params: agg.AggregateParams
+    selection: Optional[partition_selection.SelectionPlan]
+    noise_std: Dict[Any, float]
+
+
+class UtilityAnalysis:
+    """One utility-analysis run: lazy until the first report or per-partition
+    result is requested; then one pre-aggregation and one sweep pass."""
+
+    def __init__(self, col, backend, options, data_extractors, public_partitions=None):
+        _check_options(options, data_extractors)
+        if not isinstance(backend, pipeline_backend.MI355XBackend):
+            raise NotImplementedError("utility analysis runs on MI355XBackend only")
+        self.col = col
+        self.backend = backend
+        self.options = options
+        self.extractors = data_extractors
+        self.public = public_partitions
+        params = options.aggregate_params
+        acc = budget_accounting.NaiveBudgetAccountant(total_epsilon=options.epsilon,
+                                                      total_delta=options.delta)
+        mech = params.noise_kind.convert_to_mechanism_type()
+        # utility_analysis_engine.py:98-113: GENERIC first (private), then one
+        # mechanism per metric in the user's order, inside the aggregate scope
+        with acc.scope(weight=params.budget_weight):
+            self._sel_spec = (None if public_partitions is not None else
+                              acc.request_budget(agg.MechanismType.GENERIC,
+                                                 weight=params.budget_weight))
+            self._specs = {m: acc.request_budget(mech, weight=params.budget_weight)
+                           for m in params.metrics}
+        acc.compute_budgets()  # utility_analysis.py:79
+        self.metrics = [m for m, _ in _BLOCKS if m in params.metrics]
+        self.configs = [self._config(p) for p in data_structures.get_aggregate_params(options)]
+        self.strategies = data_structures.get_partition_selection_strategy(options)
+        self._done = False
+
+    # ------------------------------------------------------------ budgets
+    def _config(self, p: agg.AggregateParams) -> _Config:
+        sel = None
+        if self._sel_spec is not None:
+            sel = partition_selection.create_partition_selection_strategy(
+                p.partition_selection_strategy, self._sel_spec.eps, self._sel_spec.delta,
+                p.max_partitions_contributed, p.pre_threshold)
+        std = {}
+        l0 = p.max_partitions_contributed
+        for m in self.metrics:
+            spec = self._specs[m]
+            # per_partition_combiners.py:289-339: SUM and COUNT use linf =
+            # max_contributions_per_partition (compute_dp_count_noise_std),
+            # PRIVACY_ID_COUNT linf = 1
+            linf = 1 if m == agg.Metrics.PRIVACY_ID_COUNT else p.max_contributions_per_partition
+            std[m] = _noise_std(p.noise_kind, spec.eps, spec.delta, l0, linf)
+        return _Config(p, sel, std)
+
+    # ------------------------------------------------------------ device
+    def _pairs(self, dev):
+        """Sorted pre-aggregate (pairs, partition_start, P, key_table,
+        public bitmap)."""
+        ctx = self.backend.ctx
+        stream = torch.cuda.current_stream(dev)
+        sptr = ctypes.c_void_p(stream.cuda_stream)
+        if self.options.pre_aggregated_data:
+            return self._pairs_preaggregated(dev)
+        enc = columnar.encode(self.col, self.extractors, dev,
+                              need_values=self.extractors.value_extractor is not None,
+                              public_partitions=self.public)
+        P = enc.n_partitions
+        bound = _native.BoundParams()
+        bound.n_partitions = P
+        bound.pid_min, bound.pid_count = enc.pid_min, enc.pid_count
+        bound.rec_id_offset = enc.rec_id_offset
+        if enc.public_mask is not None:
+            bound.public_mask = enc.public_mask.data_ptr()
+        cap = max(enc.n, 1)
+        pairs = torch.empty((cap, 4), dtype=torch.float64, device=dev)  # 32 B per pair
+        starts = torch.empty(P + 1, dtype=torch.int64, device=dev)
+        with torch.cuda.device(dev):
+            n_pairs = ctx.preaggregate(
+                ctypes.c_void_p(enc.pid.data_ptr()), ctypes.c_void_p(enc.pk.data_ptr()),
+                ctypes.c_void_p(enc.value.data_ptr()) if enc.value is not None else None,
+                enc.n, bound, ctypes.c_void_p(pairs.data_ptr()), cap,
+                ctypes.c_void_p(starts.data_ptr()), sptr)
+        self.n_pairs = n_pairs
+        return pairs, starts, P, enc.key_table, enc.public_mask
+
+    def _pairs_preaggregated(self, dev):
+        """PreAggregateExtractors input: (partition key, (count, sum,
+        n_partitions)) per pair; sorted by key on ingest."""
+        rows = self.col if isinstance(self.col, list) else list(self.col)
+        ex = self.extractors
+        keys = [ex.partition_extractor(r) for r in rows]
+        pre = [ex.preaggregate_extractor(r) for r in rows]
+        ids, table, pub_ids = columnar._encode_keys(keys, torch.device("cpu"),
+                                                    None if self.public is None
+                                                    else list(self.public))
+        ids = ids.numpy()
+        P = max(len(table), 1)
+        pub_mask = None
+        if self.public is not None:
+            pub = np.zeros(P, bool)
+            pub[np.asarray(pub_ids, np.int64)] = True
+            keep = pub[ids]
+            ids, pre = ids[keep], [x for x, k in zip(pre, keep) if k]
+            bits = np.packbits(pub, bitorder="little")
+            pub_mask = torch.from_numpy(bits).to(dev)
+        order = np.argsort(ids, kind="stable")
+        n = len(order)
+        arr = np.zeros(max(n, 1), dtype=[("pk", "<u4"), ("count", "<u4"), ("sum", "<f8"),
+                                          ("np", "<u4"), ("nc", "<u4"), ("r", "<u8")])
+        if n:
+            pre_a = np.asarray(pre, dtype=np.float64).reshape(n, -1)[order]
+            arr["pk"][:n] = ids[order]
+            arr["count"][:n] = pre_a[:, 0]
+            arr["sum"][:n] = pre_a[:, 1]
+            arr["np"][:n] = pre_a[:, 2]
+        starts = np.searchsorted(ids[order], np.arange(P + 1)).astype(np.int64)
+        pairs = torch.from_numpy(arr.view(np.float64).reshape(-1, 4).copy()).to(dev)
+        self.n_pairs = n
+        return pairs, torch.from_numpy(starts).to(dev), P, table, pub_mask
+
+    def _sample_mask(self, P, key_table, dev):
+        prob = self.options.partitions_sampling_prob
+        if prob >= 1:
+            return None
+        bound = _sample_bound(prob)
+        keys = columnar.decode_keys(np.arange(P), key_table)
+        keep = np.array([_keep_by_hash(k, bound) for k in keys], bool)
+        self.sampled = keep
+        return torch.from_numpy(np.packbits(keep, bitorder="little")).to(dev)
+
+    def run(self):
+        if self._done:
+            return
+        dev = self.backend.device
+        ctx = self.backend.ctx
+        pairs, starts, P, key_table, pub_mask = self._pairs(dev)
+        sample = self._sample_mask(P, key_table, dev)
+        C = len(self.configs)
+        M = len(self.metrics)
+        cfgs = (_native.UaConfig * C)()
+        tables = []
+        for i, cf in enumerate(self.configs):
+            p = cf.params
+            x = cfgs[i]
+            x.max_partitions_contributed = p.max_partitions_contributed
+            x.max_contributions_per_partition = p.max_contributions_per_partition or 1
+            lo, hi = p.min_sum_per_partition, p.max_sum_per_partition
+            x.min_sum_per_partition = -math.inf if lo is None else float(lo)
+            x.max_sum_per_partition = math.inf if hi is None else float(hi)
+            if cf.selection is not None:
+                s = cf.selection
+                x.selection_strategy = s.native_strategy
+                x.pre_threshold = int(s.pre_threshold or 0)
+                x.threshold, x.noise_scale = s.threshold, s.noise_scale
+                if s.table is not None:
+                    t = np.ascontiguousarray(s.table, dtype=np.float64)
+                    tables.append(t)
+                    x.keep_table, x.table_len = t.ctypes.data, len(t)
+        up = _native.UaParams()
+        up.n_configs = C
+        up.metric_mask = sum(bit for m, bit in _BLOCKS if m in self.metrics)
+        up.public_partitions = int(self.public is not None)
+        up.configs = ctypes.addressof(cfgs)
+        up.sample_mask = sample.data_ptr() if sample is not None else None
+        up.public_mask = pub_mask.data_ptr() if pub_mask is not None else None
+        f64 = dict(dtype=torch.float64, device=dev)
+        raw = torch.empty((P, 2), **f64)
+        err = torch.empty((P, max(M, 1), 5, C), **f64)
+        keep = torch.empty((P, C), **f64) if self.public is None else None
+        with torch.cuda.device(dev):
+            sptr = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+            ctx.utility_analysis(ctypes.c_void_p(pairs.data_ptr()),
+                                 ctypes.c_void_p(starts.data_ptr()), P, up,
+                                 ctypes.c_void_p(raw.data_ptr()), ctypes.c_void_p(err.data_ptr()),
+                                 ctypes.c_void_p(keep.data_ptr()) if keep is not None else None,
+                                 sptr)
+        # partitions of the result: public ones, or those with pairs (and
+        # kept by partition sampling)
+        if self.public is not None:
+            bits = torch.from_numpy(np.unpackbits(pub_mask.cpu().numpy(), bitorder="little")[:P])
+            ids = torch.nonzero(bits.to(dev)).flatten()
+        else:
+            has = (starts[1:] - starts[:-1]) > 0
+            if sample is not None:
+                has &= torch.from_numpy(self.sampled).to(dev)
+            ids = torch.nonzero(has).flatten()
+        self.pairs, self.starts = pairs, starts
+        self.ids, self.key_table = ids, key_table
+        self.raw = raw[ids]
+        self.err = err[ids][:, :M]
+        self.keep = keep[ids] if keep is not None else torch.ones((len(ids), C), **f64)
+        self.stage_ms = ctx.stage_times()
+        self._done = True
+
+    # ------------------------------------------------ cross-partition combine
+    def _noise_std_tensor(self, dev):
+        return torch.tensor([[cf.noise_std[m] for cf in self.configs] for m in self.metrics],
+                            dtype=torch.float64,
+                            device=dev).reshape(len(self.metrics), len(self.configs))
+
+    def _additive_fields(self):
+        """Per (partition, configuration) additive fields of the reference's
+        CrossPartitionCombiner accumulator (cross_partition_combiners.py
+        :22-122, 146-183): [K, C, F] plus the bucket of every partition."""
+        dev = self.raw.device
+        p = self.keep                                  # [K, C]
+        w = p                                          # equal_weight_fn
+        cols = [p * 0 + 1.0, w]                        # dataset partitions, weight
+        if self.public is not None:
+            empty = (self.raw[:, 1] == 0).to(torch.float64)[:, None].expand_as(p)
+            cols += [1.0 - empty, empty]
+        else:
+            cols += [p, p * (1 - p)]
+        std = self._noise_std_tensor(dev)              # [M, C]
+        for mi in range(len(self.metrics)):
+            tot, cmin, cmax, el0, vl0 = (self.err[:, mi, f, :] for f in range(5))
+            s2 = std[mi][None, :] ** 2
+            dd_l0 = -el0
+            dd_linf = cmin - cmax
+            dd_ps = (tot - dd_l0 - dd_linf) * (1 - p)
+            mean = el0 + cmin + cmax
+            var = vl0 + s2
+            rmse = torch.sqrt(mean * mean + var)
+            rwdp = p * rmse + (1 - p) * tot.abs()
+            absf = [el0 * w, vl0 * w, cmin * w, cmax * w, mean * w, var * w, rmse * w,
+                    0 * w, rwdp * w, 0 * w]
+            nz = tot != 0
+            inv = torch.where(nz, 1.0 / torch.where(nz, tot, torch.ones_like(tot)),
+                              torch.zeros_like(tot))
+            scale = [inv, inv * inv, inv, inv, inv, inv * inv, inv, inv, inv, inv]
+            relf = [a * s for a, s in zip(absf, scale)]
+            cols += [tot, dd_l0, dd_linf, dd_ps] + absf + relf
+        F = torch.stack(cols, dim=-1)                  # [K, C, F]
+        if self.metrics:
+            size = self.err[:, 0, 0, 0]
+        else:
+            size = self.raw[:, 0]
+        bounds = torch.tensor(BUCKET_BOUNDS, dtype=torch.float64, device=dev)
+        bucket = torch.clamp(torch.searchsorted(bounds, size, right=True) - 1, min=0)
+        bucket = torch.where(size < 0, torch.zeros_like(bucket), bucket)
+        return F, bucket
+
+    def _report(self, c: int, v: np.ndarray) -> metrics.UtilityReport:
+        """UtilityReport of configuration c from its summed fields v."""
+        public = self.public is not None
+        if public:
+            info = metrics.PartitionsInfo(public_partitions=True,
+                                          num_dataset_partitions=int(round(v[2])),
+                                          num_non_public_partitions=0,
+                                          num_empty_partitions=int(round(v[3])))
+        else:
+            # the reference sets strategies[configuration_index] while the
+            # index is still -1 (utility_analysis.py:117-129 runs before
+            # :218-229 assigns it): every report names the LAST strategy
+            info = metrics.PartitionsInfo(public_partitions=False,
+                                          num_dataset_partitions=int(round(v[0])),
+                                          strategy=self.strategies[-1],
+                                          kept_partitions=metrics.MeanVariance(float(v[2]),
+                                                                               float(v[3])))
+        report = metrics.UtilityReport(configuration_index=c, partitions_info=info)
+        if not self.metrics:
+            return report
+        total_w = float(v[1])
+        wscale = 0.0 if total_w == 0 else 1.0 / total_w
+        errs = []
+        cf = self.configs[c]
+        user_metrics = list(self.options.aggregate_params.metrics)
+        for mi, m in enumerate(self.metrics):
+            b = 4 + 24 * mi
+            tot, dd = float(v[b]), v[b + 1:b + 4]
+            dscale = 1.0 if tot == 0 else 1.0 / tot
+            a, r = v[b + 4:b + 14] * wscale, v[b + 14:b + 24] * wscale
+
+            def verr(x):
+                return metrics.ValueErrors(
+                    bounding_errors=metrics.ContributionBoundingErrors(
+                        l0=metrics.MeanVariance(mean=float(x[0]), var=float(x[1])),
+                        linf_min=float(x[2]), linf_max=float(x[3])),
+                    mean=float(x[4]), variance=float(x[5]), rmse=float(x[6]), l1=float(x[7]),
+                    rmse_with_dropped_partitions=float(x[8]),
+                    l1_with_dropped_partitions=float(x[9]))
+            # the reference labels metric_errors by zipping them with the
+            # user's metric order (cross_partition_combiners.py:208-212)
+            errs.append(metrics.MetricUtility(
+                metric=user_metrics[mi], noise_std=cf.noise_std[m],
+                noise_kind=cf.params.noise_kind,
+                ratio_data_dropped=metrics.DataDropInfo(l0=float(dd[0] * dscale),
+                                                        linf=float(dd[1] * dscale),
+                                                        partition_selection=float(dd[2] * dscale)),
+                absolute_error=verr(a), relative_error=verr(r)))
+        report.metric_errors = errs
+        return report
+
+    def reports(self) -> List[metrics.UtilityReport]:
+        """One UtilityReport per configuration with its partition-size
+        histogram (utility_analysis.py:196-251)."""
+        self.run()
+        F, bucket = self._additive_fields()
+        C = len(self.configs)
+        tot = F.sum(dim=0).cpu().numpy()                       # [C, F]
+        nb = len(BUCKET_BOUNDS)
+        byb = torch.zeros((nb,) + F.shape[1:], dtype=F.dtype, device=F.device)
+        byb.index_add_(0, bucket, F)
+        present = torch.bincount(bucket, minlength=nb).cpu().numpy() > 0
+        byb = byb.cpu().numpy()
+        out = []
+        for c in range(C):
+            rep = self._report(c, tot[c])
+            hist = []
+            for bi in np.nonzero(present)[0]:
+                lo = BUCKET_BOUNDS[bi]
+                hist.append(metrics.UtilityReportBin(lo, _get_upper_bound(lo),
+                                                     self._report(c, byb[bi, c])))
+            rep.utility_report_histogram = hist if hist else None
+            out.append(rep)
+        return out
+
+    def per_partition(self) -> Iterable[Tuple[Tuple[Any, int], metrics.PerPartitionMetrics]]:
+        """((partition_key, configuration_index), PerPartitionMetrics), lazily
+        (utility_analysis.py:86-100)."""
+        self.run()
+        keys = columnar.decode_keys(self.ids.cpu().numpy(), self.key_table)
+        std = {m: [cf.noise_std[m] for cf in self.configs] for m in self.metrics}
+        C = len(self.configs)
+        chunk = 4096
+        for s in range(0, len(keys), chunk):
+            raw = self.raw[s:s + chunk].cpu().numpy()
+            err = self.err[s:s + chunk].cpu().numpy()
+            keep = self.keep[s:s + chunk].cpu().numpy()
+            for j, key in enumerate(keys[s:s + chunk]):
+                rs = metrics.RawStatistics(int(round(raw[j, 0])), int(round(raw[j, 1])))
+                for c in range(C):
+                    errs = []
+                    for mi, m in enumerate(self.metrics):
+                        e = err[j, mi, :, c]
+                        total = float(e[0]) if m == agg.Metrics.SUM else int(round(e[0]))
+                        errs.append(metrics.SumMetrics(
+                            aggregation=m, sum=total, clipping_to_min_error=float(e[1]),
+                            clipping_to_max_error=float(e[2]),
+                            expected_l0_bounding_error=float(e[3]),
+                            std_l0_bounding_error=math.sqrt(max(float(e[4]), 0.0)),
+                            std_noise=std[m][c], noise_kind=self.configs[c].params.noise_kind))
+                    prob = 1 if self.public is not None else float(keep[j, c])
+                    yield (key, c), metrics.PerPartitionMetrics(prob, rs, errs)
+
+
+class _Lazy:
+    def __init__(self, fn):
+        self._fn = fn
+
+    def __iter__(self):
+        return iter(self._fn())
+
+
+def perform_utility_analysis(col, backend, options: data_structures.UtilityAnalysisOptions,
+                             data_extractors: Union[dex.DataExtractors,
+                                                    dex.PreAggregateExtractors],
+                             public_partitions=None):
+    """Utility analysis of DP aggregations (utility_analysis.py:42-144).
+
+    Returns (reports, per_partition_result): a lazy collection with one
+    metrics.UtilityReport per configuration, and a lazy collection of
+    ((partition_key, configuration_index), metrics.PerPartitionMetrics).
+    The analysis object itself is available as `reports.analysis` for bulk
+    (tensor) access."""
+    run = UtilityAnalysis(col, backend, options, data_extractors, public_partitions)
+    reports = _Lazy(run.reports)
+    reports.analysis = run
+    per_partition = _Lazy(run.per_partition)
+    per_partition.analysis = run
+    return reports, per_partition

@@ -28,6 +28,7 @@
 #include "dpg_common.h"
 #include "dpg_partition.h"
 #include "dpg_select.h"
+#include "dpg_utility.h"
 #include "dpg_wave.h"
 
 using namespace dpg;
@@ -263,11 +264,23 @@ struct Plan {
     int64_t P;
 };
 
-// Bounding of the fine buckets + merge of the kept pairs per partition.
+// Pre-aggregate output (dpg_preaggregate): pairs sorted by partition key.
+struct PaOut {
+    ItemPA *pairs;
+    int64_t capacity;
+    int64_t *partition_start;  // [P + 1]
+    int64_t n_pairs;
+};
+
+__global__ void k_set_i64(int64_t *p, int64_t v) { *p = v; }
+
+// Bounding of the fine buckets + merge of the kept pairs per partition (or,
+// for the pre-aggregate, the pairs sorted by partition key).
 template <class R, class KeyT, class Item>
 int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
                      const int64_t *bstart, const uint32_t *bcnt, uint32_t B,
-                     const BoundParams &bp, int64_t n, const dpg_partials *out, Control *ctl) {
+                     const BoundParams &bp, int64_t n, const dpg_partials *out, Control *ctl,
+                     PaOut *pa) {
     int st = DPG_OK;
     using CL = ChunkLayout<KeyT, Item>;
     using WL = WaveLayout<KeyT, Item>;
@@ -498,32 +511,33 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     HIP_TRY(hipStreamSynchronize(s));
     if (hctl.err & 2u) return fail(ctx, DPG_ERR_HIP, "internal hash-table error in bounding");
     const int64_t n_items = hctl.item_cursor;
-    // ---- merge kept pairs per partition
-    Partials po{out->rows, out->count, out->sum, out->nsum, out->nsq};
     const int64_t P = pl.P;
-    const int64_t nranges = (P + kRange - 1) / kRange;
     constexpr int kItemIpt = sizeof(Item) == 16 ? 8 : 4;
+    // the items are partitioned by partition-key range: one level up to 1024
+    // ranges, else two (pk >> (rbits + b2), then (pk >> rbits) mod 2^b2) --
+    // the final segment index is the range id either way
+    constexpr bool kPA = ItemTraits<Item>::preagg;
+    constexpr uint32_t kRB = kPA ? 11u : (uint32_t)kRangeBits;
+    const int64_t nranges = (P + (1ll << kRB) - 1) >> kRB;
+    int64_t *baseR = nullptr;
+    uint32_t *totR = nullptr;
+    const Item *sorted = items;
+    uint32_t F = 1;
     if (n_items > 0) {
-        // partition the items by 4096-partition range: one level up to 1024
-        // ranges, else two (pk >> (12 + b2), then (pk >> 12) mod 2^b2) --
-        // the final segment index is the range id either way
         const uint32_t rb = std::max<uint32_t>(1, bits_for((uint64_t)std::max<int64_t>(1, nranges)));
         const uint32_t b2 = rb > 10 ? std::min<uint32_t>(kMaxB2, rb - 1) : 0u;
         const uint32_t b1 = rb - b2;
         const uint32_t F1 = nranges <= 1024 ? (uint32_t)std::max<int64_t>(1, nranges) : 1u << b1;
-        int64_t *baseR;
-        uint32_t *totR;
-        const Item *sorted;
         WS(items2, Item, "items2", n_items);
-        const SrcSeg<Item> src1{items, wg_pre, wg_off, G + 1, (uint32_t)kRangeBits + b2};
+        const SrcSeg<Item> src1{items, wg_pre, wg_off, G + 1, kRB + b2};
         int r = run_level<SrcSeg<Item>, Item, kItemIpt, 1024>(
             ctx, s, src1, 1u, nullptr, &ctl->item_cursor, nullptr, n_items, F1, b1, items2,
             "items", &baseR, &totR, &ctl->ntiles[4]);
         if (r) return r;
         sorted = items2;
-        uint32_t F = F1;
+        F = F1;
         if (b2 > 0) {
-            const SrcItems<Item> src2{items2, (uint32_t)kRangeBits, (1u << b2) - 1u};
+            const SrcItems<Item> src2{items2, kRB, (1u << b2) - 1u};
             int64_t *base2;
             uint32_t *tot2;
             r = run_level<SrcItems<Item>, Item, kItemIpt, 2048>(ctx, s, src2, F1, baseR, totR,
@@ -536,6 +550,34 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
             sorted = items;
             F = F1 << b2;
         }
+    }
+    if constexpr (kPA) {
+        // ---- pre-aggregate: one more level on the low 11 key bits sorts the
+        // pairs by partition key, straight into the caller's array; the
+        // digit offsets of that level are the partition starts
+        pa->n_pairs = n_items;
+        if (n_items > pa->capacity)
+            return fail(ctx, DPG_ERR_INVALID_ARG,
+                        "pairs capacity " + std::to_string(pa->capacity) + " < " +
+                            std::to_string(n_items) + " pairs");
+        if (n_items == 0) {
+            HIP_TRY(hipMemsetAsync(pa->partition_start, 0, (P + 1) * 8, s));
+            stage(ctx, s, "end");
+            return DPG_OK;
+        }
+        const SrcItems<Item> src3{sorted, 0u, (1u << kRB) - 1u};
+        int64_t *base3;
+        uint32_t *tot3;
+        int r = run_level<SrcItems<Item>, Item, kItemIpt, 2048>(
+            ctx, s, src3, F, baseR, totR, nullptr, n_items, 1u << kRB, kRB, pa->pairs, "pairs",
+            &base3, &tot3, &ctl->ntiles[7]);
+        if (r) return r;
+        HIP_TRY(hipMemcpyAsync(pa->partition_start, base3, P * 8, hipMemcpyDeviceToDevice, s));
+        k_set_i64<<<1, 1, 0, s>>>(pa->partition_start + P, n_items);
+        LAUNCH_CHECK();
+    } else if (n_items > 0) {
+        // ---- merge kept pairs per partition
+        Partials po{out->rows, out->count, out->sum, out->nsum, out->nsq};
         stage(ctx, s, "reduce");
         const int64_t rtile = 65536;
         uint32_t max_tiles = (uint32_t)(n_items / rtile + F + 1);
@@ -556,7 +598,7 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
 template <class R>
 int pipeline(dpg_ctx *ctx, hipStream_t s, const int64_t *pid, const int64_t *pk,
              const double *value, int64_t n, const dpg_bound_params *p, const dpg_partials *out,
-             Control *ctl, const Plan &pl, int64_t pid_min, uint64_t U, uint32_t ib) {
+             Control *ctl, const Plan &pl, int64_t pid_min, uint64_t U, uint32_t ib, PaOut *pa) {
     int st = DPG_OK;
     const bool var = (p->metric_mask & (DPG_M_MEAN | DPG_M_VARIANCE)) != 0;
     WS(recA, R, "recA", n);
@@ -593,15 +635,78 @@ int pipeline(dpg_ctx *ctx, hipStream_t s, const int64_t *pid, const int64_t *pk,
     bp.value = value;
     bp.err = &ctl->err;
     const bool key32 = pl.pkbits <= 21;  // (pid slot < 2^10) << pkbits | pk < 2^31
+    if (pa)
+        return key32 ? bound_and_reduce<R, uint32_t, ItemPA>(ctx, s, pl, cur, bstart, bcnt, B, bp,
+                                                             n, out, ctl, pa)
+                     : bound_and_reduce<R, uint64_t, ItemPA>(ctx, s, pl, cur, bstart, bcnt, B, bp,
+                                                             n, out, ctl, pa);
     if (var)
         return key32 ? bound_and_reduce<R, uint32_t, Item32>(ctx, s, pl, cur, bstart, bcnt, B, bp,
-                                                             n, out, ctl)
+                                                             n, out, ctl, nullptr)
                      : bound_and_reduce<R, uint64_t, Item32>(ctx, s, pl, cur, bstart, bcnt, B, bp,
-                                                             n, out, ctl);
+                                                             n, out, ctl, nullptr);
     return key32 ? bound_and_reduce<R, uint32_t, Item16>(ctx, s, pl, cur, bstart, bcnt, B, bp, n,
-                                                         out, ctl)
+                                                         out, ctl, nullptr)
                  : bound_and_reduce<R, uint64_t, Item16>(ctx, s, pl, cur, bstart, bcnt, B, bp, n,
-                                                         out, ctl);
+                                                         out, ctl, nullptr);
+}
+
+// dpg_bound_aggregate / dpg_preaggregate after argument checks: pid range,
+// level plan, record format.
+int aggregate_impl(dpg_ctx *ctx, const int64_t *pid, const int64_t *pk, const double *value,
+                   int64_t n, const dpg_bound_params *p, dpg_partials *out, PaOut *pa,
+                   hipStream_t s) {
+    int st = DPG_OK;
+    const int64_t P = p->n_partitions;
+    WS(ctl, Control, "control", 1);
+    HIP_TRY(hipMemsetAsync(ctl, 0, sizeof(Control), s));
+    {
+        Control h{};
+        h.n_scalar = n;
+        HIP_TRY(hipMemcpyAsync(&ctl->n_scalar, &h.n_scalar, 8, hipMemcpyHostToDevice, s));
+    }
+    // ---- privacy-id range
+    int64_t pid_min = p->pid_min;
+    uint64_t U = (uint64_t)p->pid_count;
+    if (U == 0) {
+        stage(ctx, s, "pidrange");
+        const unsigned long long init[2] = {~0ull, 0ull};
+        HIP_TRY(hipMemcpyAsync(&ctl->pid_lo, init, 16, hipMemcpyHostToDevice, s));
+        const int64_t blocks = std::min<int64_t>((n + 255) / 256, (int64_t)ctx->n_cu * 8);
+        k_pid_minmax<<<(unsigned)blocks, 256, 0, s>>>(pid, n, &ctl->pid_lo, &ctl->pid_hi);
+        LAUNCH_CHECK();
+        unsigned long long h[2];
+        HIP_TRY(hipMemcpyAsync(h, &ctl->pid_lo, 16, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        const int64_t lo = (int64_t)(h[0] ^ 0x8000000000000000ull);
+        const int64_t hi = (int64_t)(h[1] ^ 0x8000000000000000ull);
+        const uint64_t span = (uint64_t)hi - (uint64_t)lo;
+        if (span >= (1ull << 32))
+            return fail(ctx, DPG_ERR_KEY_RANGE, "privacy ids span more than 2^32 values");
+        pid_min = lo;
+        U = span + 1;
+    }
+    // ---- level plan: hash bits so that fine buckets average ~target records
+    Plan pl;
+    pl.P = P;
+    pl.kbits = std::max<uint32_t>(1, bits_for(U));
+    pl.pkbits = std::max<uint32_t>(1, bits_for((uint64_t)P));
+    const uint32_t target = ctx->bucket_target ? ctx->bucket_target : kBucketTarget;
+    // at most 7 pid hash bits may stay below a fine bucket (direct pid slots
+    // of a small chunk: kWCq = 128), hence the lower bound kbits - 7
+    uint32_t bits_total = bits_for((uint64_t)((n + target - 1) / target));
+    bits_total = std::max<uint32_t>(bits_total, pl.kbits > 7 ? pl.kbits - 7 : 0);
+    bits_total = std::max<uint32_t>(1, std::min<uint32_t>(bits_total, kMaxB1 + kMaxB2));
+    bits_total = std::min<uint32_t>(bits_total, pl.kbits);
+    // one level up to 11 bits; beyond, the smaller half first (level 1 reads
+    // 16 B per record, so its runs should be the longer ones)
+    pl.b1 = bits_total <= kMaxB1 ? bits_total : bits_total / 2;
+    pl.b2 = bits_total - pl.b1;
+    pl.plb = pl.kbits - bits_total;
+    const uint32_t ib = std::max<uint32_t>(1, bits_for((uint64_t)n));
+    const bool r8 = (pl.kbits - pl.b1) + pl.pkbits + ib <= 64;
+    if (r8) return pipeline<R8>(ctx, s, pid, pk, value, n, p, out, ctl, pl, pid_min, U, ib, pa);
+    return pipeline<R16>(ctx, s, pid, pk, value, n, p, out, ctl, pl, pid_min, U, ib, pa);
 }
 
 }  // namespace
@@ -687,56 +792,48 @@ int dpg_bound_aggregate(dpg_ctx *ctx, const int64_t *pid, const int64_t *pk, con
     if (out->nsum) HIP_TRY(hipMemsetAsync(out->nsum, 0, P * 8, s));
     if (out->nsq) HIP_TRY(hipMemsetAsync(out->nsq, 0, P * 8, s));
     if (n == 0) return DPG_OK;
+    return aggregate_impl(ctx, pid, pk, value, n, p, out, nullptr, s);
+}
 
-    WS(ctl, Control, "control", 1);
-    HIP_TRY(hipMemsetAsync(ctl, 0, sizeof(Control), s));
-    {
-        Control h{};
-        h.n_scalar = n;
-        HIP_TRY(hipMemcpyAsync(&ctl->n_scalar, &h.n_scalar, 8, hipMemcpyHostToDevice, s));
+int dpg_preaggregate(dpg_ctx *ctx, const int64_t *pid, const int64_t *pk, const double *value,
+                     int64_t n, const dpg_bound_params *p, dpg_pair_entry *pairs,
+                     int64_t capacity, int64_t *partition_start, int64_t *n_pairs, void *stream) {
+    static_assert(sizeof(dpg_pair_entry) == sizeof(ItemPA), "dpg_pair_entry layout");
+    if (!ctx) return DPG_ERR_INVALID_ARG;
+    if (!p || !partition_start || !n_pairs || n < 0 || (n > 0 && (!pid || !pk || !pairs)))
+        return fail(ctx, DPG_ERR_INVALID_ARG, "null argument");
+    if (p->n_partitions <= 0 || p->n_partitions >= 0xFFFFFFFFll)
+        return fail(ctx, DPG_ERR_INVALID_ARG, "n_partitions must be in [1, 2^32-1)");
+    if (n >= 0xFFFFFFFFll) return fail(ctx, DPG_ERR_UNSUPPORTED, "n must be < 2^32 per device");
+    if (p->pid_count < 0 || p->pid_count > (1ll << 32))
+        return fail(ctx, DPG_ERR_INVALID_ARG, "pid_count must be in [0, 2^32]");
+    (void)hipSetDevice(ctx->device);
+    hipStream_t s = (hipStream_t)stream;
+    ctx->stage_names.clear();
+    ctx->n_events_used = 0;
+    ctx->last_stream = s;
+    int st = DPG_OK;
+    stage(ctx, s, "begin");
+    *n_pairs = 0;
+    if (n == 0) {
+        HIP_TRY(hipMemsetAsync(partition_start, 0, (p->n_partitions + 1) * 8, s));
+        return DPG_OK;
     }
-    // ---- privacy-id range
-    int64_t pid_min = p->pid_min;
-    uint64_t U = (uint64_t)p->pid_count;
-    if (U == 0) {
-        stage(ctx, s, "pidrange");
-        const unsigned long long init[2] = {~0ull, 0ull};
-        HIP_TRY(hipMemcpyAsync(&ctl->pid_lo, init, 16, hipMemcpyHostToDevice, s));
-        const int64_t blocks = std::min<int64_t>((n + 255) / 256, (int64_t)ctx->n_cu * 8);
-        k_pid_minmax<<<(unsigned)blocks, 256, 0, s>>>(pid, n, &ctl->pid_lo, &ctl->pid_hi);
-        LAUNCH_CHECK();
-        unsigned long long h[2];
-        HIP_TRY(hipMemcpyAsync(h, &ctl->pid_lo, 16, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
-        const int64_t lo = (int64_t)(h[0] ^ 0x8000000000000000ull);
-        const int64_t hi = (int64_t)(h[1] ^ 0x8000000000000000ull);
-        const uint64_t span = (uint64_t)hi - (uint64_t)lo;
-        if (span >= (1ull << 32))
-            return fail(ctx, DPG_ERR_KEY_RANGE, "privacy ids span more than 2^32 values");
-        pid_min = lo;
-        U = span + 1;
-    }
-    // ---- level plan: hash bits so that fine buckets average ~target records
-    Plan pl;
-    pl.P = P;
-    pl.kbits = std::max<uint32_t>(1, bits_for(U));
-    pl.pkbits = std::max<uint32_t>(1, bits_for((uint64_t)P));
-    const uint32_t target = ctx->bucket_target ? ctx->bucket_target : kBucketTarget;
-    // at most 7 pid hash bits may stay below a fine bucket (direct pid slots
-    // of a small chunk: kWCq = 128), hence the lower bound kbits - 7
-    uint32_t bits_total = bits_for((uint64_t)((n + target - 1) / target));
-    bits_total = std::max<uint32_t>(bits_total, pl.kbits > 7 ? pl.kbits - 7 : 0);
-    bits_total = std::max<uint32_t>(1, std::min<uint32_t>(bits_total, kMaxB1 + kMaxB2));
-    bits_total = std::min<uint32_t>(bits_total, pl.kbits);
-    // one level up to 11 bits; beyond, the smaller half first (level 1 reads
-    // 16 B per record, so its runs should be the longer ones)
-    pl.b1 = bits_total <= kMaxB1 ? bits_total : bits_total / 2;
-    pl.b2 = bits_total - pl.b1;
-    pl.plb = pl.kbits - bits_total;
-    const uint32_t ib = std::max<uint32_t>(1, bits_for((uint64_t)n));
-    const bool r8 = (pl.kbits - pl.b1) + pl.pkbits + ib <= 64;
-    if (r8) return pipeline<R8>(ctx, s, pid, pk, value, n, p, out, ctl, pl, pid_min, U, ib);
-    return pipeline<R16>(ctx, s, pid, pk, value, n, p, out, ctl, pl, pid_min, U, ib);
+    // no bounding: every pair kept, values summed unclipped
+    dpg_bound_params q = *p;
+    q.mode = DPG_MODE_CROSS_PARTITION;
+    q.sum_mode = value ? DPG_SUM_CLIP_PARTITION : DPG_SUM_NONE;
+    q.metric_mask = value ? (DPG_M_COUNT | DPG_M_SUM) : DPG_M_COUNT;
+    q.max_partitions_contributed = 0x7FFFFFFF;
+    q.max_contributions_per_partition = 0x7FFFFFFF;
+    q.max_contributions = 0;
+    q.min_sum_per_partition = -HUGE_VAL;
+    q.max_sum_per_partition = HUGE_VAL;
+    PaOut pa{reinterpret_cast<ItemPA *>(pairs), capacity, partition_start, 0};
+    dpg_partials none{};
+    const int rc = aggregate_impl(ctx, pid, pk, value, n, &q, &none, &pa, s);
+    *n_pairs = pa.n_pairs;
+    return rc;
 }
 
 int dpg_select_and_noise(dpg_ctx *ctx, const dpg_partials *in, const dpg_select_params *sel,
@@ -818,6 +915,102 @@ int dpg_compact_kept(dpg_ctx *ctx, const uint8_t *keep, const double *out, int64
     LAUNCH_CHECK();
     HIP_TRY(hipMemcpyAsync(n_kept, tot, 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
+    return DPG_OK;
+}
+
+int dpg_utility_analysis(dpg_ctx *ctx, const dpg_pair_entry *pairs,
+                         const int64_t *partition_start, int64_t P, const dpg_ua_params *u,
+                         double *raw, double *errors, double *keep, void *stream) {
+    if (!ctx) return DPG_ERR_INVALID_ARG;
+    if (!u || !partition_start || !raw || !errors || !u->configs || P <= 0)
+        return fail(ctx, DPG_ERR_INVALID_ARG, "null argument");
+    if (u->n_configs < 1 || u->n_configs > 64)
+        return fail(ctx, DPG_ERR_INVALID_ARG, "n_configs must be in [1, 64]");
+    if (!u->public_partitions && !keep)
+        return fail(ctx, DPG_ERR_INVALID_ARG, "private partitions need the keep output");
+    if (u->public_partitions && !u->public_mask)
+        return fail(ctx, DPG_ERR_INVALID_ARG, "public partitions need public_mask");
+    (void)hipSetDevice(ctx->device);
+    hipStream_t s = (hipStream_t)stream;
+    int st = DPG_OK;
+    const int C = u->n_configs;
+    UaArgs a{};
+    a.n_configs = C;
+    a.has_sum = (u->metric_mask & DPG_M_SUM) != 0;
+    a.has_count = (u->metric_mask & DPG_M_COUNT) != 0;
+    a.has_pid = (u->metric_mask & DPG_M_PRIVACY_ID_COUNT) != 0;
+    a.n_metrics = a.has_sum + a.has_count + a.has_pid;
+    a.P = P;
+    // configurations and keep tables to the device
+    std::vector<UaConfig> hc(C);
+    std::vector<double> tabs;
+    for (int i = 0; i < C; ++i) {
+        const dpg_ua_config &x = u->configs[i];
+        if (x.max_partitions_contributed <= 0 || x.max_contributions_per_partition <= 0)
+            return fail(ctx, DPG_ERR_INVALID_ARG, "contribution bounds must be positive");
+        UaConfig &y = hc[i];
+        y.mpc = (double)x.max_partitions_contributed;
+        y.mcpp = (double)x.max_contributions_per_partition;
+        y.lo = x.min_sum_per_partition;
+        y.hi = x.max_sum_per_partition;
+        y.strategy = x.selection_strategy;
+        y.pre_threshold = (int32_t)x.pre_threshold;
+        y.threshold = x.threshold;
+        y.scale = x.noise_scale;
+        y.table_offset = (int64_t)tabs.size();
+        y.table_len = 0;
+        if (!u->public_partitions && x.selection_strategy == DPG_SELECT_TRUNCATED_GEOMETRIC) {
+            if (!x.keep_table || x.table_len <= 0)
+                return fail(ctx, DPG_ERR_INVALID_ARG, "truncated geometric needs keep_table");
+            tabs.insert(tabs.end(), x.keep_table, x.keep_table + x.table_len);
+            y.table_len = x.table_len;
+        }
+    }
+    WS(dcfg, UaConfig, "ua.cfg", C);
+    HIP_TRY(hipMemcpyAsync(dcfg, hc.data(), sizeof(UaConfig) * C, hipMemcpyHostToDevice, s));
+    a.cfg = dcfg;
+    if (!tabs.empty()) {
+        WS(dtab, double, "ua.tables", tabs.size());
+        HIP_TRY(hipMemcpyAsync(dtab, tabs.data(), 8 * tabs.size(), hipMemcpyHostToDevice, s));
+        a.tables = dtab;
+    }
+    a.sample_mask = u->sample_mask;
+    a.public_mask = u->public_partitions ? u->public_mask : nullptr;
+    WS(mom, double, "ua.mom", (size_t)P * kUaMom * C);
+    a.raw = raw;
+    a.err = errors;
+    a.mom = mom;
+    a.keep = keep;
+    HIP_TRY(hipMemsetAsync(raw, 0, (size_t)P * 2 * 8, s));
+    HIP_TRY(hipMemsetAsync(errors, 0, (size_t)P * a.n_metrics * 5 * C * 8, s));
+    HIP_TRY(hipMemsetAsync(mom, 0, (size_t)P * kUaMom * C * 8, s));
+    if (keep) HIP_TRY(hipMemsetAsync(keep, 0, (size_t)P * C * 8, s));
+    int64_t n = 0;
+    HIP_TRY(hipMemcpyAsync(&n, partition_start + P, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    stage(ctx, s, "ua.accumulate");
+    if (n > 0) {
+        const int64_t runs = (n + kUaRun - 1) / kUaRun;
+        if (runs >= 0x7FFFFFFF) return fail(ctx, DPG_ERR_UNSUPPORTED, "too many pairs");
+        k_ua_accumulate<<<(unsigned)runs, 64, 0, s>>>(reinterpret_cast<const ItemPA *>(pairs),
+                                                      partition_start, n, a);
+        LAUNCH_CHECK();
+    }
+    if (u->public_partitions) {
+        const unsigned g = (unsigned)std::min<int64_t>(P, (int64_t)ctx->n_cu * 16);
+        k_ua_public<<<g, 64, 0, s>>>(a);
+        LAUNCH_CHECK();
+    } else if (n > 0) {
+        stage(ctx, s, "ua.select");
+        const size_t lds = (size_t)(kUaMaxExact + 1) * 64 * 8;
+        (void)hipFuncSetAttribute((const void *)k_ua_select,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        const unsigned g = (unsigned)std::min<int64_t>(P, (int64_t)ctx->n_cu * 3 * 8);
+        k_ua_select<<<g, 64, lds, s>>>(reinterpret_cast<const ItemPA *>(pairs), partition_start,
+                                       a);
+        LAUNCH_CHECK();
+    }
+    stage(ctx, s, "ua.end");
     return DPG_OK;
 }
 

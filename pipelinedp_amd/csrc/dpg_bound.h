@@ -114,10 +114,20 @@ struct ItemTraits;
 template <>
 struct ItemTraits<Item16> {
     static constexpr bool var = false;
+    static constexpr bool preagg = false;
 };
 template <>
 struct ItemTraits<Item32> {
     static constexpr bool var = true;
+    static constexpr bool preagg = false;
+};
+// utility-analysis pre-aggregate: every pair kept (the host passes no-op
+// bounds), each pair also carries its privacy id's partition and record
+// counts (analysis/contribution_bounders.py:37-77)
+template <>
+struct ItemTraits<ItemPA> {
+    static constexpr bool var = false;
+    static constexpr bool preagg = true;
 };
 
 __device__ __forceinline__ uint32_t hslot(uint32_t key, uint32_t mask) {
@@ -271,6 +281,7 @@ __global__ __launch_bounds__(kBigThreads) void k_bound_big(
     const size_t *scratch_off, char *scratch, BoundParams bp, Item *items, const int64_t *item_off,
     uint32_t *item_cursor) {
     constexpr bool kVar = ItemTraits<Item>::var;
+    constexpr bool kPA = ItemTraits<Item>::preagg;
     __shared__ uint32_t sh_bump, sh_bump2;
     const uint32_t b = blockIdx.x;
     const int tid = threadIdx.x;
@@ -339,6 +350,7 @@ __global__ __launch_bounds__(kBigThreads) void k_bound_big(
             insert_key<uint64_t>(pairtab, Cp - 1, ((uint64_t)qs << pkb) | pk, wp, bp.err);
         atomicAdd(&paircnt[ps], 1u);
         if (!per_pid && wp) atomicAdd(&pidm[qs], 1u);
+        if (kPA) atomicAdd(&pidc[qs], 1u);  // records per pid (no pid is over a limit)
         rqs[i] = qs;
         rps[i] = ps;
     }
@@ -500,6 +512,12 @@ __global__ __launch_bounds__(kBigThreads) void k_bound_big(
         if constexpr (kVar) {
             it.nsum = need_v ? acc_nsum[p] : 0.0;
             it.nsq = need_v ? acc_nsq[p] : 0.0;
+        }
+        if constexpr (kPA) {
+            const uint32_t q = (uint32_t)(pkey >> pkb);
+            it.npart = pidm[q];
+            it.ncontrib = pidc[q];
+            it.pad0 = it.pad1 = 0;
         }
         out[atomicAdd(item_cursor, 1u)] = it;
     }

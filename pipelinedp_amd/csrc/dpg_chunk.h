@@ -250,10 +250,14 @@ __device__ __forceinline__ void bound_chunk(const R (&r)[kRPT], uint32_t n, uint
         for (int k = 0; k < kRPT; ++k) {
             if (valid[k]) atomicAdd(&paircnt[ps[k]], 1u);
             const bool touch = per_pid ? valid[k] : won[k];
-            oldm[k] = atomicAdd(&pidm[qs[k]], touch ? 1u : 0u);
+            // pre-aggregate: records per pid in the high half (no pid is
+            // over a limit, so no candidate appends use it)
+            const uint32_t rec = (ItemTraits<Item>::preagg && valid[k]) ? 1u << 16 : 0u;
+            oldm[k] = atomicAdd(&pidm[qs[k]], (touch ? 1u : 0u) + rec);
         }
 #pragma unroll
-        for (int k = 0; k < kRPT; ++k) first[k] = (per_pid ? valid[k] : won[k]) && oldm[k] == 0u;
+        for (int k = 0; k < kRPT; ++k)
+            first[k] = (per_pid ? valid[k] : won[k]) && (oldm[k] & 0xFFFFu) == 0u;
         uint32_t qi[kRPT], li[kRPT];
         wave_alloc_batch<kRPT>(&sh->npid, first, qi);
         wave_alloc_batch<kRPT>(&sh->npair, won, li);
@@ -512,6 +516,12 @@ __device__ __forceinline__ void bound_chunk(const R (&r)[kRPT], uint32_t n, uint
         if constexpr (kVar) {
             it.nsum = need_v ? acc_nsum[p] : 0.0;
             it.nsq = need_v ? acc_nsq[p] : 0.0;
+        }
+        if constexpr (ItemTraits<Item>::preagg) {
+            const uint32_t pm = pidm[(uint32_t)(pairtab[p] >> pkb) & (kCq - 1)];
+            it.npart = pm & 0xFFFFu;
+            it.ncontrib = pm >> 16;
+            it.pad0 = it.pad1 = 0;
         }
         items[slot] = it;
     }

@@ -81,6 +81,15 @@ struct alignas(16) Item32 {  // one kept pair with MEAN / VARIANCE moments
     double nsq;
 };
 
+struct alignas(16) ItemPA {  // one (pid, pk) pair of the utility-analysis pre-aggregate
+    uint32_t pk;
+    uint32_t cnt;       // records of the pair
+    double sum;         // sum of their values (unclipped)
+    uint32_t npart;     // partitions the privacy id contributes to
+    uint32_t ncontrib;  // records of the privacy id
+    uint32_t pad0, pad1;
+};
+
 // ------------------------------------------------------------ privacy-id hash
 // A bijection on [0, 2^bits): xorshift / odd-multiply rounds (the Murmur3
 // finaliser's shape, shifts scaled to the width).  The top bits pick the

@@ -344,7 +344,14 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
 #pragma unroll
         for (int k = 0; k < kWRPT; ++k) {
             if ((validm >> k) & 1u) atomicAdd(&pcnt[dn[k]], 1u);
-            if ((touchm >> k) & 1u) atomicAdd(&pidm[qs[k]], 1u);
+            if constexpr (ItemTraits<Item>::preagg) {
+                // pre-aggregate: records per pid in the high half (no pid is
+                // over a limit, so no candidate appends use it)
+                if ((validm >> k) & 1u)
+                    atomicAdd(&pidm[qs[k]], (1u << 16) + ((touchm >> k) & 1u));
+            } else {
+                if ((touchm >> k) & 1u) atomicAdd(&pidm[qs[k]], 1u);
+            }
         }
     }
     // pid_hash of every pid slot of the chunk's residual range: 2 per lane,
@@ -693,6 +700,12 @@ bool overp[kWQPL];
                 if constexpr (kVar) {
                     it.nsum = a1[j];
                     it.nsq = a2[j];
+                }
+                if constexpr (ItemTraits<Item>::preagg) {
+                    const uint32_t pm = pidm[(uint32_t)(pkv[j] >> pkb) & (kWCq - 1)];
+                    it.npart = pm & 0xFFFFu;
+                    it.ncontrib = pm >> 16;
+                    it.pad0 = it.pad1 = 0;
                 }
                 items[nitems + lanes_below(be)] = it;
             }

@@ -37,14 +37,20 @@ def test_struct_layouts_match_c(tmp_path):
                    'sizeof(dpg_bound_params), sizeof(dpg_partials), sizeof(dpg_select_params),'
                    'sizeof(dpg_noise_params), offsetof(dpg_bound_params, public_mask),'
                    'offsetof(dpg_select_params, public_mask), offsetof(dpg_noise_params, msq_const_value),'
-                   'offsetof(dpg_bound_params, rec_id_offset));}')
+                   'offsetof(dpg_bound_params, rec_id_offset));'
+                   'printf("%zu %zu %zu %zu %zu\\n", sizeof(dpg_pair_entry), sizeof(dpg_ua_config),'
+                   'sizeof(dpg_ua_params), offsetof(dpg_ua_config, keep_table),'
+                   'offsetof(dpg_ua_params, public_mask));}')
     exe = tmp_path / "layout"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
     got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
     want = [ctypes.sizeof(_native.BoundParams), ctypes.sizeof(_native.Partials),
             ctypes.sizeof(_native.SelectParams), ctypes.sizeof(_native.NoiseParams),
             _native.BoundParams.public_mask.offset, _native.SelectParams.public_mask.offset,
-            _native.NoiseParams.msq_const_value.offset, _native.BoundParams.rec_id_offset.offset]
+            _native.NoiseParams.msq_const_value.offset, _native.BoundParams.rec_id_offset.offset,
+            ctypes.sizeof(_native.PairEntry), ctypes.sizeof(_native.UaConfig),
+            ctypes.sizeof(_native.UaParams), _native.UaConfig.keep_table.offset,
+            _native.UaParams.public_mask.offset]
     assert got == want
 
 
