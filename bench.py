@@ -289,12 +289,119 @@ def _launch_ranks(n: int) -> int:
     return subprocess.call(cmd)
 
 
+def _ua_options(n_side: int = 8):
+    """configs[4]: 64 MultiParameterConfiguration rows, mpc x mcpp in
+    {1, 2, 4, ..., 128}^2, COUNT + SUM + PRIVACY_ID_COUNT, private selection."""
+    import pipelinedp_amd as pdp
+    from pipelinedp_amd import analysis
+    vals = [2**i for i in range(n_side)]
+    mpc = [a for a in vals for _ in vals]
+    mcpp = [b for _ in vals for b in vals]
+    multi = analysis.MultiParameterConfiguration(
+        max_partitions_contributed=mpc, max_contributions_per_partition=mcpp,
+        min_sum_per_partition=[0.0] * len(mpc), max_sum_per_partition=[10.0 * b for b in mcpp])
+    params = pdp.AggregateParams(
+        metrics=[pdp.Metrics.COUNT, pdp.Metrics.SUM, pdp.Metrics.PRIVACY_ID_COUNT],
+        noise_kind=pdp.NoiseKind.LAPLACE, max_partitions_contributed=1,
+        max_contributions_per_partition=1, min_sum_per_partition=0.0, max_sum_per_partition=10.0)
+    return analysis.UtilityAnalysisOptions(epsilon=1.0, delta=1e-6, aggregate_params=params,
+                                           multi_param_configuration=multi), mpc, mcpp
+
+
+def _ua_cpu_baseline(n_records: int, P: int):
+    """The utility-analysis oracle (numpy/Python, one core) on a small sample
+    of the same generator and the same 64 configurations."""
+    from oracle import utility_oracle as uo
+    _, mpc, mcpp = _ua_options()
+    n_pid = max(1, n_records // 100)
+    pid, pk, val = host_sample(n_records, n_pid, P, 7)
+    cfgs = [dict(mpc=a, mcpp=b, min_sum=0.0, max_sum=10.0 * b, noise_kind="LAPLACE",
+                 strategy="TRUNCATED_GEOMETRIC", pre_threshold=None) for a, b in zip(mpc, mcpp)]
+    t0 = time.perf_counter()
+    pairs = uo.preaggregate(pid.tolist(), pk.tolist(), val.tolist())
+    uo.analyze(pairs, cfgs, ["COUNT", "SUM", "PRIVACY_ID_COUNT"], 1.0, 1e-6, "LAPLACE")
+    dt = time.perf_counter() - t0
+    return {"value": n_records / dt, "unit": "records/s", "cores": 1, "kind": "port",
+            "sample": f"{n_records} records, {n_pid} privacy ids, {P} partitions, 64 "
+                      f"configurations; oracle/utility_oracle.py (numpy + Python loops) "
+                      f"pre-aggregation + per-partition + cross-partition, {dt:.1f} s"}
+
+
+def bench_config5(args):
+    """configs[4]: utility-analysis sweep of 64 contribution-bound
+    configurations over 1e9 records in one device pass (pre-aggregate +
+    per-partition sweep + cross-partition reports), single GPU."""
+    import pipelinedp_amd as pdp
+    from pipelinedp_amd import analysis
+    if args.gpus != 1:
+        raise SystemExit("config5 runs on one GPU (the sweep does not shard)")
+    P = args.partitions or 1_000_000
+    cpu = None if args.no_cpu_baseline else _ua_cpu_baseline(20_000, 200)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    pid, pk, val = generate(args.records, args.pids, P, 0, 1, dev)
+    torch.cuda.synchronize()
+    backend = pdp.MI355XBackend(device=0, seed=0xD1FF5EED)
+    cols = pdp.ColumnarData(pid=pid, pk=pk, value=val, n_partitions=P,
+                            privacy_id_range=(0, args.pids))
+    opts, _, _ = _ua_options()
+    ex = pdp.DataExtractors("pid", "pk", "value")
+
+    def step():
+        reports, _ = analysis.perform_utility_analysis(cols, backend, opts, ex)
+        return list(reports), reports.analysis
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    stage_tot = {}
+    for _ in range(args.steps):
+        reps, run = step()
+        for k, v in run.stage_ms.items():
+            stage_tot[k] = stage_tot.get(k, 0.0) + v
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    dev_ms = ev0.elapsed_time(ev1) / args.steps
+    ms = wall / args.steps * 1e3
+    C = len(reps)
+    algo = ALGO_BYTES_PER_RECORD * args.records + C * P * 40
+    achieved = algo / (dev_ms * 1e-3) / 1e9
+    line = {
+        "metric": METRIC, "value": args.records / (wall / args.steps), "unit": "records/s",
+        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (device-generated Zipf keys, uniform values)",
+        "config": {"workload": f"configs[4]: utility-analysis sweep of {C} configurations "
+                               f"(mpc x mcpp in {{1..128}}^2) over {args.records:.0e} records / "
+                               f"{args.pids:.0e} privacy ids / {P:.0e} Zipf(1.1) partitions, "
+                               "COUNT+SUM+PRIVACY_ID_COUNT, private selection",
+                   "records": args.records, "partitions": P, "configurations": C,
+                   "pairs": int(run.n_pairs), "parallelism": "single GPU"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "device_ms": dev_ms,
+                     "kernel": "whole sweep (dpg_preaggregate + dpg_utility_analysis + "
+                               "cross-partition combine)",
+                     "note": "achieved = (24 B x records + configurations x partitions x 40 B) "
+                             "/ device time per step (SURVEY.md 8(d))"},
+        "stage_ms": {k: v / args.steps for k, v in stage_tot.items()},
+        "lib_sha256": _lib_sha(),
+    }
+    if cpu is not None:
+        line["cpu_baseline"] = cpu
+    print(json.dumps(line), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=["config2", "config4"], default="config2")
+    ap.add_argument("--workload", choices=["config2", "config4", "config5"], default="config2")
     ap.add_argument("--public", action="store_true",
                     help="config4: public_partitions = range(P) instead of private selection")
     ap.add_argument("--records", type=int, default=1_000_000_000)
@@ -309,6 +416,8 @@ def main():
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(_launch_ranks(args.gpus))
+    if args.workload == "config5":
+        return bench_config5(args)
     c4 = args.workload == "config4"
     if args.partitions is None:
         args.partitions = 100_000_000 if c4 else 1_000_000

@@ -201,6 +201,9 @@ typedef struct dpg_ua_config {
     int64_t table_len;
     double threshold;            /* Laplace / Gaussian thresholding        */
     double noise_scale;
+    double noise_std[3];         /* report: noise std of SUM, COUNT and
+                                    PRIVACY_ID_COUNT (compute_dp_count_noise_std,
+                                    dp_computations.py:369-395)             */
 } dpg_ua_config;
 
 typedef struct dpg_ua_params {
@@ -287,12 +290,21 @@ int dpg_preaggregate(dpg_ctx *ctx, const int64_t *pid, const int64_t *pk, const 
  *          clipping_to_max_error, expected_l0_bounding_error and the l0
  *          bounding variance (SumMetrics before the noise std is attached)
  *   keep   double[P][C]: partition_selection_probability_to_keep (NULL for
- *          public partitions).
- * Partitions outside sample_mask or without pairs (and not public) stay 0. */
+ *          public partitions)
+ *   report double[29][F][C] or NULL: the cross-partition combine
+ *          (analysis/cross_partition_combiners.py:264-343) summed per
+ *          partition-size bucket (utility_analysis.py:29-39, 182-251), F =
+ *          4 + 24 M fields: partitions, weight, 2 partition-info terms, then
+ *          per metric its sum, 3 data-drop terms and 10 absolute + 10
+ *          relative error terms, weighted by the keep probability; dividing
+ *          by the weight / metric sums gives the UtilityReport
+ *   *n_out (host, optional) receives the number of output partitions.
+ * Partitions outside sample_mask or without pairs (and not public) stay 0
+ * and are not in the output. */
 int dpg_utility_analysis(dpg_ctx *ctx, const dpg_pair_entry *pairs,
                          const int64_t *partition_start, int64_t n_partitions,
                          const dpg_ua_params *params, double *raw, double *errors, double *keep,
-                         void *stream);
+                         double *report, int64_t *n_out, void *stream);
 
 /* Timing/profiling aid: per-stage device time (ms) of the last
  * dpg_bound_aggregate call, measured with HIP events on its stream.

@@ -74,7 +74,7 @@ class UaConfig(ctypes.Structure):
                 ("selection_strategy", ctypes.c_int32), ("reserved", ctypes.c_int32),
                 ("pre_threshold", ctypes.c_int64), ("keep_table", ctypes.c_void_p),
                 ("table_len", ctypes.c_int64), ("threshold", ctypes.c_double),
-                ("noise_scale", ctypes.c_double)]
+                ("noise_scale", ctypes.c_double), ("noise_std", ctypes.c_double * 3)]
 
 
 class UaParams(ctypes.Structure):
@@ -152,7 +152,7 @@ def load():
                                          i64, vp, ctypes.POINTER(ctypes.c_int64), vp]
         lib.dpg_preaggregate.restype = ctypes.c_int
         lib.dpg_utility_analysis.argtypes = [vp, vp, vp, i64, ctypes.POINTER(UaParams), vp, vp,
-                                             vp, vp]
+                                             vp, vp, ctypes.POINTER(ctypes.c_int64), vp]
         lib.dpg_utility_analysis.restype = ctypes.c_int
         lib.dpg_last_stage_times.argtypes = [vp, ctypes.c_char_p, ctypes.c_size_t,
                                              ctypes.POINTER(ctypes.c_double), i32,
@@ -237,11 +237,13 @@ class Context:
         return n_pairs.value
 
     def utility_analysis(self, pairs_ptr, starts_ptr, n_partitions, params: UaParams, raw_ptr,
-                         err_ptr, keep_ptr, stream):
+                         err_ptr, keep_ptr, report_ptr, stream) -> int:
+        n_out = ctypes.c_int64(0)
         st = self.lib.dpg_utility_analysis(self.handle, pairs_ptr, starts_ptr, n_partitions,
                                            ctypes.byref(params), raw_ptr, err_ptr, keep_ptr,
-                                           stream)
+                                           report_ptr, ctypes.byref(n_out), stream)
         self.check(st, "dpg_utility_analysis")
+        return n_out.value
 
     def stage_times(self):
         names = ctypes.create_string_buffer(1024)

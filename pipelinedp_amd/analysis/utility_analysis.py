@@ -277,85 +277,46 @@ class UtilityAnalysis:
         up.configs = ctypes.addressof(cfgs)
         up.sample_mask = sample.data_ptr() if sample is not None else None
         up.public_mask = pub_mask.data_ptr() if pub_mask is not None else None
+        slot = {agg.Metrics.SUM: 0, agg.Metrics.COUNT: 1, agg.Metrics.PRIVACY_ID_COUNT: 2}
+        for i, cf in enumerate(self.configs):
+            for m in self.metrics:
+                cfgs[i].noise_std[slot[m]] = cf.noise_std[m]
         f64 = dict(dtype=torch.float64, device=dev)
         raw = torch.empty((P, 2), **f64)
         err = torch.empty((P, max(M, 1), 5, C), **f64)
         keep = torch.empty((P, C), **f64) if self.public is None else None
+        F = 4 + 24 * M
+        rep = torch.empty((len(BUCKET_BOUNDS), F, C), **f64)
         with torch.cuda.device(dev):
             sptr = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-            ctx.utility_analysis(ctypes.c_void_p(pairs.data_ptr()),
-                                 ctypes.c_void_p(starts.data_ptr()), P, up,
-                                 ctypes.c_void_p(raw.data_ptr()), ctypes.c_void_p(err.data_ptr()),
-                                 ctypes.c_void_p(keep.data_ptr()) if keep is not None else None,
-                                 sptr)
-        # partitions of the result: public ones, or those with pairs (and
-        # kept by partition sampling)
-        if self.public is not None:
-            bits = torch.from_numpy(np.unpackbits(pub_mask.cpu().numpy(), bitorder="little")[:P])
-            ids = torch.nonzero(bits.to(dev)).flatten()
-        else:
-            has = (starts[1:] - starts[:-1]) > 0
-            if sample is not None:
-                has &= torch.from_numpy(self.sampled).to(dev)
-            ids = torch.nonzero(has).flatten()
-        self.pairs, self.starts = pairs, starts
-        self.ids, self.key_table = ids, key_table
-        self.raw = raw[ids]
-        self.err = err[ids][:, :M]
-        self.keep = keep[ids] if keep is not None else torch.ones((len(ids), C), **f64)
+            self.n_out = ctx.utility_analysis(
+                ctypes.c_void_p(pairs.data_ptr()), ctypes.c_void_p(starts.data_ptr()), P, up,
+                ctypes.c_void_p(raw.data_ptr()), ctypes.c_void_p(err.data_ptr()),
+                ctypes.c_void_p(keep.data_ptr()) if keep is not None else None,
+                ctypes.c_void_p(rep.data_ptr()), sptr)
+        self.pairs, self.starts, self.key_table = pairs, starts, key_table
+        self.sample, self.pub_mask = sample, pub_mask
+        self.raw_all, self.err_all, self.keep_all, self.rep = raw, err, keep, rep
         self.stage_ms = ctx.stage_times()
         self._done = True
 
-    # ------------------------------------------------ cross-partition combine
-    def _noise_std_tensor(self, dev):
-        return torch.tensor([[cf.noise_std[m] for cf in self.configs] for m in self.metrics],
-                            dtype=torch.float64,
-                            device=dev).reshape(len(self.metrics), len(self.configs))
-
-    def _additive_fields(self):
-        """Per (partition, configuration) additive fields of the reference's
-        CrossPartitionCombiner accumulator (cross_partition_combiners.py
-        :22-122, 146-183): [K, C, F] plus the bucket of every partition."""
-        dev = self.raw.device
-        p = self.keep                                  # [K, C]
-        w = p                                          # equal_weight_fn
-        cols = [p * 0 + 1.0, w]                        # dataset partitions, weight
+    def output_ids(self) -> torch.Tensor:
+        """Dense ids of the result's partitions: the public ones, or those
+        with pairs (and kept by partition sampling)."""
+        P = self.starts.numel() - 1
+        dev = self.starts.device
         if self.public is not None:
-            empty = (self.raw[:, 1] == 0).to(torch.float64)[:, None].expand_as(p)
-            cols += [1.0 - empty, empty]
-        else:
-            cols += [p, p * (1 - p)]
-        std = self._noise_std_tensor(dev)              # [M, C]
-        for mi in range(len(self.metrics)):
-            tot, cmin, cmax, el0, vl0 = (self.err[:, mi, f, :] for f in range(5))
-            s2 = std[mi][None, :] ** 2
-            dd_l0 = -el0
-            dd_linf = cmin - cmax
-            dd_ps = (tot - dd_l0 - dd_linf) * (1 - p)
-            mean = el0 + cmin + cmax
-            var = vl0 + s2
-            rmse = torch.sqrt(mean * mean + var)
-            rwdp = p * rmse + (1 - p) * tot.abs()
-            absf = [el0 * w, vl0 * w, cmin * w, cmax * w, mean * w, var * w, rmse * w,
-                    0 * w, rwdp * w, 0 * w]
-            nz = tot != 0
-            inv = torch.where(nz, 1.0 / torch.where(nz, tot, torch.ones_like(tot)),
-                              torch.zeros_like(tot))
-            scale = [inv, inv * inv, inv, inv, inv, inv * inv, inv, inv, inv, inv]
-            relf = [a * s for a, s in zip(absf, scale)]
-            cols += [tot, dd_l0, dd_linf, dd_ps] + absf + relf
-        F = torch.stack(cols, dim=-1)                  # [K, C, F]
-        if self.metrics:
-            size = self.err[:, 0, 0, 0]
-        else:
-            size = self.raw[:, 0]
-        bounds = torch.tensor(BUCKET_BOUNDS, dtype=torch.float64, device=dev)
-        bucket = torch.clamp(torch.searchsorted(bounds, size, right=True) - 1, min=0)
-        bucket = torch.where(size < 0, torch.zeros_like(bucket), bucket)
-        return F, bucket
+            bits = np.unpackbits(self.pub_mask.cpu().numpy(), bitorder="little")[:P]
+            return torch.nonzero(torch.from_numpy(bits).to(dev)).flatten()
+        has = (self.starts[1:] - self.starts[:-1]) > 0
+        if self.sample is not None:
+            has &= torch.from_numpy(self.sampled).to(dev)
+        return torch.nonzero(has).flatten()
 
+    # ------------------------------------------------ cross-partition combine
     def _report(self, c: int, v: np.ndarray) -> metrics.UtilityReport:
-        """UtilityReport of configuration c from its summed fields v."""
+        """UtilityReport of configuration c from its summed fields v (the
+        field layout of dpg_utility_analysis' report output)."""
         public = self.public is not None
         if public:
             info = metrics.PartitionsInfo(public_partitions=True,
@@ -407,24 +368,18 @@ class UtilityAnalysis:
 
     def reports(self) -> List[metrics.UtilityReport]:
         """One UtilityReport per configuration with its partition-size
-        histogram (utility_analysis.py:196-251)."""
+        histogram (utility_analysis.py:196-251), from the device's summed
+        report fields per (size bucket, configuration)."""
         self.run()
-        F, bucket = self._additive_fields()
-        C = len(self.configs)
-        tot = F.sum(dim=0).cpu().numpy()                       # [C, F]
-        nb = len(BUCKET_BOUNDS)
-        byb = torch.zeros((nb,) + F.shape[1:], dtype=F.dtype, device=F.device)
-        byb.index_add_(0, bucket, F)
-        present = torch.bincount(bucket, minlength=nb).cpu().numpy() > 0
-        byb = byb.cpu().numpy()
+        byb = self.rep.permute(0, 2, 1).cpu().numpy()        # [bucket, C, F]
+        present = byb[:, 0, 0] > 0
+        tot = byb.sum(axis=0)                                 # [C, F]
         out = []
-        for c in range(C):
+        for c in range(len(self.configs)):
             rep = self._report(c, tot[c])
-            hist = []
-            for bi in np.nonzero(present)[0]:
-                lo = BUCKET_BOUNDS[bi]
-                hist.append(metrics.UtilityReportBin(lo, _get_upper_bound(lo),
-                                                     self._report(c, byb[bi, c])))
+            hist = [metrics.UtilityReportBin(BUCKET_BOUNDS[bi], _get_upper_bound(BUCKET_BOUNDS[bi]),
+                                             self._report(c, byb[bi, c]))
+                    for bi in np.nonzero(present)[0]]
             rep.utility_report_histogram = hist if hist else None
             out.append(rep)
         return out
@@ -433,14 +388,17 @@ class UtilityAnalysis:
         """((partition_key, configuration_index), PerPartitionMetrics), lazily
         (utility_analysis.py:86-100)."""
         self.run()
-        keys = columnar.decode_keys(self.ids.cpu().numpy(), self.key_table)
+        ids = self.output_ids()
+        keys = columnar.decode_keys(ids.cpu().numpy(), self.key_table)
         std = {m: [cf.noise_std[m] for cf in self.configs] for m in self.metrics}
         C = len(self.configs)
+        M = len(self.metrics)
         chunk = 4096
         for s in range(0, len(keys), chunk):
-            raw = self.raw[s:s + chunk].cpu().numpy()
-            err = self.err[s:s + chunk].cpu().numpy()
-            keep = self.keep[s:s + chunk].cpu().numpy()
+            sel = ids[s:s + chunk]
+            raw = self.raw_all[sel].cpu().numpy()
+            err = self.err_all[sel][:, :M].cpu().numpy()
+            keep = self.keep_all[sel].cpu().numpy() if self.keep_all is not None else None
             for j, key in enumerate(keys[s:s + chunk]):
                 rs = metrics.RawStatistics(int(round(raw[j, 0])), int(round(raw[j, 1])))
                 for c in range(C):
@@ -454,7 +412,7 @@ class UtilityAnalysis:
                             expected_l0_bounding_error=float(e[3]),
                             std_l0_bounding_error=math.sqrt(max(float(e[4]), 0.0)),
                             std_noise=std[m][c], noise_kind=self.configs[c].params.noise_kind))
-                    prob = 1 if self.public is not None else float(keep[j, c])
+                    prob = 1 if keep is None else float(keep[j, c])
                     yield (key, c), metrics.PerPartitionMetrics(prob, rs, errs)
 
 

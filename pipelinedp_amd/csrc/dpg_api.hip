@@ -920,7 +920,8 @@ int dpg_compact_kept(dpg_ctx *ctx, const uint8_t *keep, const double *out, int64
 
 int dpg_utility_analysis(dpg_ctx *ctx, const dpg_pair_entry *pairs,
                          const int64_t *partition_start, int64_t P, const dpg_ua_params *u,
-                         double *raw, double *errors, double *keep, void *stream) {
+                         double *raw, double *errors, double *keep, double *report,
+                         int64_t *n_out, void *stream) {
     if (!ctx) return DPG_ERR_INVALID_ARG;
     if (!u || !partition_start || !raw || !errors || !u->configs || P <= 0)
         return fail(ctx, DPG_ERR_INVALID_ARG, "null argument");
@@ -987,6 +988,7 @@ int dpg_utility_analysis(dpg_ctx *ctx, const dpg_pair_entry *pairs,
     if (keep) HIP_TRY(hipMemsetAsync(keep, 0, (size_t)P * C * 8, s));
     int64_t n = 0;
     HIP_TRY(hipMemcpyAsync(&n, partition_start + P, 8, hipMemcpyDeviceToHost, s));
+    if (n_out) *n_out = 0;
     HIP_TRY(hipStreamSynchronize(s));
     stage(ctx, s, "ua.accumulate");
     if (n > 0) {
@@ -1002,13 +1004,50 @@ int dpg_utility_analysis(dpg_ctx *ctx, const dpg_pair_entry *pairs,
         LAUNCH_CHECK();
     } else if (n > 0) {
         stage(ctx, s, "ua.select");
-        const size_t lds = (size_t)(kUaMaxExact + 1) * 64 * 8;
-        (void)hipFuncSetAttribute((const void *)k_ua_select,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        const unsigned g = (unsigned)std::min<int64_t>(P, (int64_t)ctx->n_cu * 3 * 8);
-        k_ua_select<<<g, 64, lds, s>>>(reinterpret_cast<const ItemPA *>(pairs), partition_start,
-                                       a);
+        const unsigned g = (unsigned)std::min<int64_t>(P, (int64_t)ctx->n_cu * 16);
+        k_ua_select<<<g, 64, 0, s>>>(reinterpret_cast<const ItemPA *>(pairs), partition_start, a);
         LAUNCH_CHECK();
+    }
+    if (report) {
+        // ---- cross-partition report sums per (size bucket, configuration)
+        stage(ctx, s, "ua.report");
+        std::vector<double> hs((size_t)std::max(1, a.n_metrics) * C, 0.0);
+        int mi = 0;
+        for (int bit : {DPG_M_SUM, DPG_M_COUNT, DPG_M_PRIVACY_ID_COUNT}) {
+            if (!(u->metric_mask & bit)) continue;
+            const int slot = bit == DPG_M_SUM ? 0 : (bit == DPG_M_COUNT ? 1 : 2);
+            for (int i = 0; i < C; ++i) hs[(size_t)mi * C + i] = u->configs[i].noise_std[slot];
+            ++mi;
+        }
+        WS(dstd, double, "ua.std", hs.size());
+        HIP_TRY(hipMemcpyAsync(dstd, hs.data(), 8 * hs.size(), hipMemcpyHostToDevice, s));
+        WS(bucket, int32_t, "ua.bucket", P);
+        WS(bcount, uint32_t, "ua.bcount", kUaBuckets);
+        WS(order, int64_t, "ua.order", P);
+        a.std = dstd;
+        a.bucket = bucket;
+        a.bcount = bcount;
+        a.order = order;
+        a.rep = report;
+        const int F = 4 + 24 * a.n_metrics;
+        HIP_TRY(hipMemsetAsync(bcount, 0, 4 * kUaBuckets, s));
+        HIP_TRY(hipMemsetAsync(report, 0, (size_t)kUaBuckets * F * C * 8, s));
+        const unsigned gb = (unsigned)std::min<int64_t>((P + 255) / 256, (int64_t)ctx->n_cu * 8);
+        k_ua_bucket<<<gb, 256, 0, s>>>(partition_start, a);
+        LAUNCH_CHECK();
+        uint32_t hc[kUaBuckets];
+        HIP_TRY(hipMemcpyAsync(hc, bcount, sizeof(hc), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        uint32_t run = 0, start[kUaBuckets];
+        for (int b = 0; b < kUaBuckets; ++b) start[b] = run, run += hc[b];
+        HIP_TRY(hipMemcpyAsync(bcount, start, sizeof(start), hipMemcpyHostToDevice, s));
+        k_ua_order<<<gb, 256, 0, s>>>(a);
+        LAUNCH_CHECK();
+        if (run > 0) {
+            k_ua_report<<<(unsigned)((run + kUaRepRun - 1) / kUaRepRun), 64, 0, s>>>((int64_t)run, a);
+            LAUNCH_CHECK();
+        }
+        if (n_out) *n_out = run;
     }
     stage(ctx, s, "ua.end");
     return DPG_OK;

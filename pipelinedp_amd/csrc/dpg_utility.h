@@ -19,7 +19,7 @@
 //   k_ua_public: public partitions get the empty accumulator every public
 //     partition carries in the reference (dp_engine.py:288-303).
 //   k_ua_select: one wave per partition: the exact Poisson-binomial PMF of
-//     the privacy-id count (<= 100 pairs; LDS column per lane) or its refined
+//     the privacy-id count (<= 100 pairs; coefficients in registers) or its refined
 //     normal approximation from the moments, dotted with the keep
 //     probability of the configuration's selection strategy.
 #pragma once
@@ -39,6 +39,10 @@ struct UaConfig {                     // device copy of dpg_ua_config
     double threshold, scale;
 };
 
+constexpr int kUaBuckets = 29;        // utility_analysis.py:29-39 bucket bounds
+constexpr int kUaRepRun = 512;        // partitions per report wave
+constexpr int kUaMaxF = 4 + 24 * 3;   // report fields per configuration
+
 struct UaArgs {
     int32_t n_configs;
     int32_t has_sum, has_count, has_pid;  // metric blocks present (in this order)
@@ -52,6 +56,12 @@ struct UaArgs {
     double *err;                      // [P][n_metrics][5][C]
     double *mom;                      // [P][3][C]
     double *keep;                     // [P][C]
+    // cross-partition report (k_ua_bucket / k_ua_order / k_ua_report)
+    const double *std;                // [n_metrics][C] noise std of each metric
+    int32_t *bucket;                  // [P] size bucket of an output partition, -1 else
+    uint32_t *bcount;                 // [kUaBuckets] partitions per bucket, then cursors
+    int64_t *order;                   // partitions of the output, bucket by bucket
+    double *rep;                      // [kUaBuckets][F][C] summed report fields
 };
 
 __device__ __forceinline__ bool bit_of(const uint8_t *m, int64_t k) {
@@ -199,36 +209,58 @@ __device__ __forceinline__ double ua_pi(const UaConfig &cf, const double *tables
     return 0.5 * erfc(-z * 0.70710678118654752440);
 }
 
+// out-of-line copy for the fully unrolled exact-PMF dot product (keeps the
+// unrolled body small, so the coefficient array stays in registers)
+__device__ __attribute__((noinline)) double ua_pi_call(const UaConfig &cf, const double *tables,
+                                                       int64_t i) {
+    return ua_pi(cf, tables, i);
+}
+
 // refined normal approximation (poisson_binomial.py:61-83)
 __device__ __forceinline__ double ua_G(double x, double skew) {
     const double phi = 0.39894228040143267794 * exp(-0.5 * x * x);
     return 0.5 * erfc(-x * 0.70710678118654752440) + skew * (1.0 - x * x) * phi / 6.0;
 }
 
+constexpr int kPgfB = 8;                                  // coefficients per block
+constexpr int kPgfNB = (kUaMaxExact + kPgfB) / kPgfB;     // 13 blocks: 104 >= 101
+
 __global__ __launch_bounds__(64) void k_ua_select(const ItemPA *pairs, const int64_t *pstart,
                                                   UaArgs a) {
-    extern __shared__ __attribute__((aligned(16))) double s_pgf[];  // [kUaMaxExact + 1][64]
     const int c = (int)__lane_id();
     const int64_t C64 = a.n_configs;
     const bool lane_on = c < a.n_configs;
     const UaConfig cf = a.cfg[lane_on ? c : 0];
-    double *col = s_pgf + c;  // lane-private column, stride 64
     for (int64_t k = blockIdx.x; k < a.P; k += gridDim.x) {
         const int64_t b = pstart[k], n = pstart[k + 1] - b;
         if (n == 0 || (a.sample_mask && !bit_of(a.sample_mask, k))) continue;
         double keep = 0.0;
         if (n <= kUaMaxExact) {
-            // exact PMF: coefficients of prod_j (1 - p_j + p_j x)
-            col[0] = 1.0;
+            // exact PMF: coefficients of prod_j (1 - p_j + p_j x) in registers;
+            // pair j touches coefficients 0..j+1 only, so blocks above that
+            // are skipped (j is wave-uniform: uniform branches)
+            double co[kPgfB * kPgfNB];
+#pragma unroll
+            for (int i = 0; i < kPgfB * kPgfNB; ++i) co[i] = i == 0 ? 1.0 : 0.0;
             for (int64_t j = 0; j < n; ++j) {
                 const uint32_t np = pairs[b + j].npart;
                 const double p = np > 0 ? fmin(1.0, cf.mpc / (double)np) : 0.0;
-                col[64 * (j + 1)] = 0.0;
-                for (int64_t i = j + 1; i >= 1; --i)
-                    col[64 * i] = col[64 * i] * (1.0 - p) + col[64 * (i - 1)] * p;
-                col[0] *= 1.0 - p;
+                const double q = 1.0 - p;
+                const int top = (int)j + 1;
+#pragma unroll
+                for (int bb = kPgfNB - 1; bb >= 0; --bb) {
+                    if (bb * kPgfB > top) continue;
+#pragma unroll
+                    for (int t = kPgfB - 1; t >= 0; --t) {
+                        const int i = bb * kPgfB + t;
+                        if (i == 0) co[0] *= q;
+                        else co[i] = co[i] * q + co[i - 1] * p;
+                    }
+                }
             }
-            for (int64_t i = 0; i <= n; ++i) keep += col[64 * i] * ua_pi(cf, a.tables, i);
+#pragma unroll
+            for (int i = 0; i < kPgfB * kPgfNB; ++i)
+                if (i <= n) keep += co[i] * ua_pi_call(cf, a.tables, i);
         } else {
             const double *mm = a.mom + k * kUaMom * C64 + (lane_on ? c : 0);
             const double mean = mm[0], sd = sqrt(mm[C64]);
@@ -249,6 +281,151 @@ __global__ __launch_bounds__(64) void k_ua_select(const ItemPA *pairs, const int
         }
         if (lane_on) a.keep[k * C64 + c] = keep;
     }
+}
+
+// ---------------------------------------------------------------- report
+// Cross-partition combine (cross_partition_combiners.py:264-343 and the
+// size histogram of utility_analysis.py:182-251): per (size bucket,
+// configuration) the sums of the CrossPartitionCombiner accumulator fields
+//   [0] partitions, [1] weight (= keep probability), [2..3] partition info
+//   (kept mean / variance, or non-empty / empty public partitions), then per
+//   metric: sum, 3 data-drop terms, 10 absolute and 10 relative error terms
+//   (weighted); the host divides by the weight and the metric sums.
+__device__ __forceinline__ int ua_bucket_of(double n) {
+    // index of the largest bound <= n (bounds 0, 1, 10, 20, 50, 100, ...)
+    if (!(n >= 1.0)) return 0;
+    int b = 1;
+    double base = 10.0;
+    for (int i = 0; i < 9; ++i, base *= 10.0) {
+        if (n >= base) b = 2 + 3 * i;
+        if (n >= 2.0 * base) b = 3 + 3 * i;
+        if (n >= 5.0 * base) b = 4 + 3 * i;
+    }
+    return b;
+}
+
+__device__ __forceinline__ bool ua_in_output(const UaArgs &a, const int64_t *pstart, int64_t k) {
+    if (a.public_mask) return bit_of(a.public_mask, k);
+    return pstart[k + 1] > pstart[k] && !(a.sample_mask && !bit_of(a.sample_mask, k));
+}
+
+__global__ __launch_bounds__(256) void k_ua_bucket(const int64_t *pstart, UaArgs a) {
+    __shared__ uint32_t h[kUaBuckets];
+    if (threadIdx.x < kUaBuckets) h[threadIdx.x] = 0;
+    __syncthreads();
+    const int64_t C64 = a.n_configs;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < a.P;
+         k += (int64_t)gridDim.x * blockDim.x) {
+        int b = -1;
+        if (ua_in_output(a, pstart, k)) {
+            const double size = a.n_metrics ? a.err[k * a.n_metrics * 5 * C64] : a.raw[2 * k];
+            b = ua_bucket_of(size);
+            atomicAdd(&h[b], 1u);
+        }
+        a.bucket[k] = b;
+    }
+    __syncthreads();
+    if (threadIdx.x < kUaBuckets && h[threadIdx.x]) atomicAdd(&a.bcount[threadIdx.x], h[threadIdx.x]);
+}
+
+// bcount holds each bucket's start: every output partition takes a slot of
+// its bucket (one atomic per distinct bucket of a wave)
+__global__ __launch_bounds__(256) void k_ua_order(UaArgs a) {
+    const uint32_t lane = __lane_id();
+    for (int64_t k0 = (int64_t)blockIdx.x * blockDim.x; k0 < a.P;
+         k0 += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t k = k0 + threadIdx.x;
+        const int b = k < a.P ? a.bucket[k] : -1;
+        uint64_t todo = __ballot(b >= 0);
+        while (todo) {
+            const int l = __builtin_ctzll(todo);
+            const int bb = __builtin_amdgcn_readlane(b, l);
+            const uint64_t same = __ballot(b == bb) & todo;
+            uint32_t base = 0;
+            if ((int)lane == l) base = atomicAdd(&a.bcount[bb], (uint32_t)__popcll(same));
+            base = __builtin_amdgcn_readlane(base, l);
+            if ((same >> lane) & 1ull)
+                a.order[base + __popcll(same & ((1ull << lane) - 1ull))] = k;
+            todo &= ~same;
+        }
+    }
+}
+
+__global__ __launch_bounds__(64) void k_ua_report(int64_t K, UaArgs a) {
+    const int64_t lo = (int64_t)blockIdx.x * kUaRepRun;
+    if (lo >= K) return;
+    const int64_t hi = lo + kUaRepRun < K ? lo + kUaRepRun : K;
+    const int c = (int)__lane_id();
+    const int C = a.n_configs;
+    const int64_t C64 = C;
+    const bool on = c < C;
+    const int cc = on ? c : 0;
+    const int M = a.n_metrics;
+    const int F = 4 + 24 * M;
+    double acc[kUaMaxF];
+#pragma unroll
+    for (int f = 0; f < kUaMaxF; ++f) acc[f] = 0.0;
+    double s2[3];
+#pragma unroll
+    for (int m = 0; m < 3; ++m) s2[m] = m < M ? a.std[m * C64 + cc] * a.std[m * C64 + cc] : 0.0;
+    int cur = a.bucket[a.order[lo]];
+    auto flush = [&](int b) {
+        if (!on) return;
+        double *o = a.rep + (int64_t)b * F * C64 + c;
+#pragma unroll
+        for (int f = 0; f < kUaMaxF; ++f)
+            if (f < F) atomicAdd(o + f * C64, acc[f]);
+    };
+    for (int64_t i = lo; i < hi; ++i) {
+        const int64_t k = a.order[i];
+        const int b = a.bucket[k];
+        if (b != cur) {
+            flush(cur);
+#pragma unroll
+            for (int f = 0; f < kUaMaxF; ++f) acc[f] = 0.0;
+            cur = b;
+        }
+        const double p = a.public_mask ? 1.0 : a.keep[k * C64 + cc];
+        acc[0] += 1.0;
+        acc[1] += p;
+        if (a.public_mask) {
+            const double empty = a.raw[2 * k + 1] == 0.0 ? 1.0 : 0.0;
+            acc[2] += 1.0 - empty;
+            acc[3] += empty;
+        } else {
+            acc[2] += p;
+            acc[3] += p * (1.0 - p);
+        }
+#pragma unroll
+        for (int m = 0; m < 3; ++m) {
+            if (m >= M) break;
+            const double *e = a.err + (k * M + m) * 5 * C64 + cc;
+            const double tot = e[0], cmin = e[C64], cmax = e[2 * C64], el0 = e[3 * C64],
+                         vl0 = e[4 * C64];
+            const double w = p;
+            const double dl0 = -el0, dlinf = cmin - cmax;
+            const double mean = el0 + cmin + cmax, var = vl0 + s2[m];
+            const double rmse = sqrt(mean * mean + var);
+            const double rwdp = p * rmse + (1.0 - p) * fabs(tot);
+            const double ab[8] = {el0 * w, vl0 * w, cmin * w, cmax * w, mean * w, var * w,
+                                  rmse * w, rwdp * w};
+            const double inv = tot != 0.0 ? 1.0 / tot : 0.0;
+            const double sc[8] = {inv, inv * inv, inv, inv, inv, inv * inv, inv, inv};
+            double *q = acc + 4 + 24 * m;
+            q[0] += tot;
+            q[1] += dl0;
+            q[2] += dlinf;
+            q[3] += (tot - dl0 - dlinf) * (1.0 - p);
+            // absolute errors (l1 terms stay 0), then relative ones
+            const int ia[8] = {0, 1, 2, 3, 4, 5, 6, 8};
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                q[4 + ia[t]] += ab[t];
+                q[14 + ia[t]] += ab[t] * sc[t];
+            }
+        }
+    }
+    flush(cur);
 }
 
 }  // namespace dpg

@@ -24,6 +24,7 @@ library behind PyDP (python-dp==1.1.4); no reference test pins them
 n = 12, pre = 3 behaves as n = 10 in the same test).
 """
 import dataclasses
+import functools
 import math
 from typing import Optional
 
@@ -38,7 +39,10 @@ def adjusted_delta(delta: float, l0: int) -> float:
     return -math.expm1(math.log1p(-delta) / l0)
 
 
-def truncated_geometric_table(eps: float, delta: float, l0: int):
+@functools.lru_cache(maxsize=64)
+def truncated_geometric_table(eps: float, delta: float, l0: int) -> tuple:
+    """pi(0..) until it reaches 1 (cached: a sweep asks for the same (eps,
+    delta, l0) many times)."""
     e = eps / l0
     d = adjusted_delta(delta, l0)
     grow, shrink = math.exp(e), math.exp(-e)
@@ -46,7 +50,14 @@ def truncated_geometric_table(eps: float, delta: float, l0: int):
     while table[-1] < 1.0 and len(table) < _MAX_TABLE:
         q = table[-1]
         table.append(min(grow * q + d, 1.0 + shrink * (q + d - 1.0), 1.0))
-    return table
+    if table[-1] < 1.0:
+        # the kernel keeps every partition with n >= len(table): refuse rather
+        # than keep partitions near the cap with probability 1
+        raise ValueError(
+            f"truncated geometric partition selection: eps / l0 = {e:.3g} needs more than "
+            f"{_MAX_TABLE} keep-table entries; use a larger epsilon or a smaller "
+            f"max_partitions_contributed")
+    return tuple(table)
 
 
 def _inverse_std_normal_cdf(p: float) -> float:

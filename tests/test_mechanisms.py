@@ -104,3 +104,13 @@ def test_sensitivities():
         dpc.Sensitivities(l0=1, linf=0)
     s = dpc.Sensitivities(l0=4, linf=2)
     assert (s.l1, s.l2) == (8, 4.0)
+
+
+def test_truncated_geometric_table_refuses_to_truncate():
+    """a table that would stop below 1 at the 2^22 cap raises
+    instead of keeping partitions past the cap with probability 1."""
+    from pipelinedp_amd import partition_selection as ps
+    t = ps.truncated_geometric_table(1.0, 1e-6, 4)
+    assert t[-1] == 1.0 and t[0] == 0.0
+    with pytest.raises(ValueError, match="keep-table"):
+        ps.truncated_geometric_table(1e-3, 1e-12, 1000)
