@@ -211,6 +211,11 @@ __device__ __forceinline__ uint32_t cand_threshold_e(uint32_t m, float e) {
     if (e >= (float)m) return 0xFFFFFFFFu;
     return (uint32_t)(e / (float)m * 4294967040.0f);
 }
+// the same, for m pairs whose priorities are known to lie in [0, B]
+__device__ __forceinline__ uint32_t cand_threshold_be(uint32_t m, float e, uint32_t B) {
+    if (e >= (float)m) return 0xFFFFFFFFu;
+    return (uint32_t)((float)B * (e / (float)m));
+}
 __device__ __forceinline__ uint32_t cand_threshold(uint32_t m, uint32_t k) {
     const float e = (float)k + 3.0f * sqrtf((float)k) + 3.0f;
     if (e >= (float)m) return 0xFFFFFFFFu;

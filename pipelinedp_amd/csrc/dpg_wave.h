@@ -52,7 +52,8 @@ struct WaveLayout {
     static constexpr size_t PIDSLOT = PIDM + 4 * kWCq;  // pool base (+ appends << 16) or kNil
     // pair key table (kWCk slots); once every insert has settled, a slot
     // holds its pair's dense id instead of the key
-    static constexpr size_t KEYS = PIDSLOT + 4 * kWCq;
+    static constexpr size_t CBND = PIDSLOT + 4 * kWCq;  // candidate bound per pid slot
+    static constexpr size_t KEYS = CBND + 4 * kWCq;
     static constexpr size_t PKEY = KEYS + sizeof(KeyT) * kWCk;  // dense: pair key
     static constexpr size_t PCNT = PKEY + sizeof(KeyT) * kWCp;  // dense: records
     static constexpr size_t PST = PCNT + 4 * kWCp;              // dense: state
@@ -69,10 +70,13 @@ struct WaveLayout {
 };
 
 #ifndef DPG_RT_W
-#define DPG_RT_W 4
+#define DPG_RT_W 8
 #endif
 #ifndef DPG_E0_C
 #define DPG_E0_C 2.0f
+#endif
+#ifndef DPG_CAND_C
+#define DPG_CAND_C 2.0f
 #endif
 
 // Compiler-level ordering of one wave's LDS accesses between phases (the
@@ -217,24 +221,131 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
     const bool part_clip = bp.sum_mode == DPG_SUM_CLIP_PARTITION;
     const uint32_t lim = per_pid ? bp.L : bp.mpc;
     const uint32_t hshift = f.kbits - f.b1;
-    const uint32_t kn = (n + 63) >> 6;  // occupied record slots per lane (uniform)
+    uint32_t kn = (n + 63) >> 6;  // occupied record slots per lane (uniform)
 
+    // ---- A-: candidate pre-filter (cross-partition modes).  A pair's
+    // priority is a function of (pid, pk), so every record of a pair shares
+    // it: records whose priority is above a per-pid bound belong to pairs
+    // the mpc sample can only keep if fewer than mpc pairs lie below it.
+    // The bound aims at ~DPG_CAND_C x (mpc + 2 sqrt(mpc) + 2) records per
+    // pid, so only those records are inserted into the pair table; a pid
+    // left short of mpc candidate pairs restarts the chunk with every record
+    // (rare).  Pids with <= mpc records keep all of them.
+    uint32_t qs[kWRPT], dn[kWRPT];
+    uint32_t validm = 0;  // per-lane bit k: record slot occupied
+    uint32_t insm = 0;    // records inserted into the pair table
+    uint32_t npair = 0;
+    uint32_t *cbnd = reinterpret_cast<uint32_t *>(smem + L::CBND);
+#pragma unroll
+    for (int k = 0; k < kWRPT && k < (int)kn; ++k) {
+        validm |= lane + 64u * k < n ? 1u << k : 0u;
+        qs[k] = ((uint32_t)(RecOps<R>::key(r[k], f) >> pkb) - hbase) & (kWCq - 1);
+    }
+    if constexpr (!kPerPid) {
+#pragma unroll
+        for (int k = 0; k < kWRPT && k < (int)kn; ++k)
+            if ((validm >> k) & 1u) atomicAdd(&pidslot[qs[k]], 1u);  // records per pid
+        wave_sync();
+    }
+    // pid_hash of every pid slot of the chunk's residual range: 2 per lane,
+    // no first-toucher detection (slots without a pid get a value nobody
+    // reads); the candidate bound from the pid's record count
+    if constexpr (!kPerPid) {
+        // occupied slots only (typically a handful): compacted into lanes
+        const float cmul = DPG_CAND_C * ((float)bp.mpc + 2.0f * sqrtf((float)bp.mpc) + 2.0f);
+        uint32_t *olist = reinterpret_cast<uint32_t *>(pool);
+        uint32_t nocc = 0;
+#pragma unroll
+        for (int j = 0; j < kWQPL; ++j) {
+            const uint32_t q = lane + 64u * j;
+            const bool occ = pidslot[q] > 0;
+            const uint64_t bo = __ballot(occ);
+            if (occ) olist[nocc + lanes_below(bo)] = q;
+            else cbnd[q] = 0xFFFFFFFFu;
+            nocc += (uint32_t)__popcll(bo);
+        }
+        wave_sync();
+        for (uint32_t o = 0; o < nocc; o += 64) {
+            if (o + lane < nocc) {
+                const uint32_t q = olist[o + lane];
+                pidv[q] = pid_hash(bp.seed, (uint64_t)(bp.pid_min + (int64_t)hk_inv(
+                                                           (d1 << hshift) | (hbase + q), bp.hash)));
+                const uint32_t rc = pidslot[q];
+                const float fr = cmul / (float)rc;
+                cbnd[q] = rc <= bp.mpc || fr >= 1.0f ? 0xFFFFFFFFu
+                                                     : (uint32_t)(fr * 4294967296.0f);
+            }
+        }
+    } else {
+        // pid_hash of every pid slot of the chunk's residual range: 2 per
+        // lane (slots without a pid get a value nobody reads)
+#pragma unroll
+        for (int j = 0; j < kWQPL; ++j) {
+            const uint32_t q = lane + 64u * j;
+            pidv[q] = pid_hash(bp.seed, (uint64_t)(bp.pid_min + (int64_t)hk_inv(
+                                                                     (d1 << hshift) | (hbase + q), bp.hash)));
+        }
+    }
+    wave_sync();
+    if constexpr (!kPerPid) {
+        uint32_t pv[kWRPT], cb[kWRPT];
+#pragma unroll
+        for (int k = 0; k < kWRPT && k < (int)kn; ++k) {
+            pv[k] = pidv[qs[k]];
+            cb[k] = cbnd[qs[k]];
+        }
+#pragma unroll
+        for (int k = 0; k < kWRPT && k < (int)kn; ++k) {
+            const uint32_t pk = (uint32_t)(RecOps<R>::key(r[k], f) & pkmask);
+            if (((validm >> k) & 1u) && pair_prio_h(pv[k], pk) <= cb[k]) insm |= 1u << k;
+        }
+    } else {
+        insm = validm;
+    }
+    // the candidates, compacted into the first slots (pool + accumulator
+    // area: idle until phase A), are the records the phases below work on;
+    // a restart switches back to all of them
+    R cur[kWRPT];
+    uint32_t ncand = n;
+    if constexpr (!kPerPid) {
+        R *lst = reinterpret_cast<R *>(pool);
+        static_assert(8 * kWPool + 8 * kWCp >= sizeof(R) * kWCap, "candidate list");
+        ncand = 0;
+#pragma unroll
+        for (int k = 0; k < kWRPT && k < (int)kn; ++k) {
+            const bool c = (insm >> k) & 1u;
+            const uint64_t bc = __ballot(c);
+            if (c) lst[ncand + lanes_below(bc)] = r[k];
+            ncand += (uint32_t)__popcll(bc);
+        }
+        wave_sync();
+#pragma unroll
+        for (int k = 0; k < kWRPT; ++k)
+            if (64u * k < ncand) cur[k] = lst[min(lane + 64u * k, ncand - 1)];
+        wave_sync();
+    }
     // ---- A: pair inserts: home-slot CAS of all records in flight; a record
     // whose home holds another key tries a second slot (other bits of the same
     // hash), then probes linearly from there -- one probe step of all of them
     // per round (table load <= 1/2; both choices taken ~ load^2)
-    uint32_t qs[kWRPT], dn[kWRPT];
-    uint32_t validm = 0;  // per-lane bit k
-    uint32_t npair = 0;
-    {
+    for (uint32_t round = (kPerPid || ncand == 0) ? 1u : 0u;; ++round) {
+        // round 0: the compacted candidates; round 1: every record
+        const uint32_t nn = round ? n : ncand;
+        kn = (nn + 63) >> 6;
+        validm = 0;
+#pragma unroll
+        for (int k = 0; k < kWRPT && k < (int)kn; ++k) {
+            if (round) cur[k] = r[k];
+            validm |= lane + 64u * k < nn ? 1u << k : 0u;
+            qs[k] = ((uint32_t)(RecOps<R>::key(cur[k], f) >> pkb) - hbase) & (kWCq - 1);
+        }
+        insm = validm;
         uint32_t ps[kWRPT], alt[kWRPT], wonm = 0;
         KeyT pkey[kWRPT], op[kWRPT];
 #pragma unroll
-        for (int k = 0; k < kWRPT; ++k) {
-            const bool valid = lane + 64u * k < n;
-            validm |= valid ? 1u << k : 0u;
-            const uint64_t key = RecOps<R>::key(r[k], f);
-            qs[k] = ((uint32_t)(key >> pkb) - hbase) & (kWCq - 1);
+        for (int k = 0; k < kWRPT && k < (int)kn; ++k) {
+            const bool valid = (insm >> k) & 1u;
+            const uint64_t key = RecOps<R>::key(cur[k], f);
             pkey[k] = ((KeyT)qs[k] << pkb) | (KeyT)(key & pkmask);
             const uint32_t hh = hslot(pkey[k], 0xFFFFFFFFu);
             ps[k] = hh & (kWCk - 1);
@@ -245,8 +356,8 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
         mark(bp, 0, clk);
         uint32_t pend = 0;
 #pragma unroll
-        for (int k = 0; k < kWRPT; ++k) {
-            if (!((validm >> k) & 1u)) continue;
+        for (int k = 0; k < kWRPT && k < (int)kn; ++k) {
+            if (!((insm >> k) & 1u)) continue;
             if (op[k] == empty_key<KeyT>()) wonm |= 1u << k;
             else if (op[k] != pkey[k]) pend |= 1u << k;
         }
@@ -262,7 +373,7 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
             uint32_t *cres = pst;
             uint32_t npend = 0;
 #pragma unroll
-            for (int k = 0; k < kWRPT; ++k) {
+            for (int k = 0; k < kWRPT && k < (int)kn; ++k) {
                 const bool pk_ = (pend >> k) & 1u;
                 const uint64_t b = __ballot(pk_);
                 if (pk_) {
@@ -303,9 +414,9 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
                 wave_sync();
                 uint32_t res[kWRPT];
 #pragma unroll
-                for (int k = 0; k < kWRPT; ++k) res[k] = cres[lane + 64u * k];
+                for (int k = 0; k < kWRPT && k < (int)kn; ++k) res[k] = cres[lane + 64u * k];
 #pragma unroll
-                for (int k = 0; k < kWRPT; ++k) {
+                for (int k = 0; k < kWRPT && k < (int)kn; ++k) {
                     if ((pend >> k) & 1u) {
                         ps[k] = res[k] & (kWCk - 1);
                         if (res[k] & 0x8000u) wonm |= 1u << k;
@@ -316,7 +427,7 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
         mark(bp, 9, clk);
         // winners: dense pair ids (the probing is over: slots now hold ids)
 #pragma unroll
-        for (int k = 0; k < kWRPT; ++k) {
+        for (int k = 0; k < kWRPT && k < (int)kn; ++k) {
             const bool won = (wonm >> k) & 1u;
             const uint64_t bw = __ballot(won);
             if (won) {
@@ -337,31 +448,42 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
         }
         wave_sync();
 #pragma unroll
-        for (int k = 0; k < kWRPT; ++k) dn[k] = min((uint32_t)keys[ps[k]], kWCp - 1);
+        for (int k = 0; k < kWRPT && k < (int)kn; ++k) dn[k] = min((uint32_t)keys[ps[k]], kWCp - 1);
         // counts: records per pair; pairs (records in PER_PRIVACY_ID mode)
         // per pid
-        const uint32_t touchm = per_pid ? validm : wonm;
+        const uint32_t touchm = per_pid ? insm : wonm;
 #pragma unroll
-        for (int k = 0; k < kWRPT; ++k) {
-            if ((validm >> k) & 1u) atomicAdd(&pcnt[dn[k]], 1u);
+        for (int k = 0; k < kWRPT && k < (int)kn; ++k) {
+            if ((insm >> k) & 1u) atomicAdd(&pcnt[dn[k]], 1u);
             if constexpr (ItemTraits<Item>::preagg) {
                 // pre-aggregate: records per pid in the high half (no pid is
                 // over a limit, so no candidate appends use it)
-                if ((validm >> k) & 1u)
+                if ((insm >> k) & 1u)
                     atomicAdd(&pidm[qs[k]], (1u << 16) + ((touchm >> k) & 1u));
             } else {
                 if ((touchm >> k) & 1u) atomicAdd(&pidm[qs[k]], 1u);
             }
         }
-    }
-    // pid_hash of every pid slot of the chunk's residual range: 2 per lane,
-    // no first-toucher detection (slots without a pid get a value nobody
-    // reads)
+        if (kPerPid || round > 0) break;
+        // a pid with more than mpc records but fewer than mpc candidate pairs
+        // may own kept pairs above its bound: restart with every record
+        wave_sync();
+        bool shrt = false;
 #pragma unroll
-    for (int j = 0; j < kWQPL; ++j) {
-        const uint32_t q = lane + 64u * j;
-        pidv[q] = pid_hash(bp.seed, (uint64_t)(bp.pid_min + (int64_t)hk_inv(
-                                                                 (d1 << hshift) | (hbase + q), bp.hash)));
+        for (int j = 0; j < kWQPL; ++j) {
+            const uint32_t q = lane + 64u * j;
+            shrt |= cbnd[q] != 0xFFFFFFFFu && (pidm[q] & 0xFFFFu) < bp.mpc;
+        }
+        if (!__ballot(shrt)) break;
+        // restart: clear the pair table and the pair counts per pid
+        constexpr int kClr0 = (int)(sizeof(KeyT) * kWCk / (16 * 64));
+#pragma unroll
+        for (int i = 0; i < kClr0; ++i)
+            reinterpret_cast<uint4 *>(keys)[lane + 64u * i] = make_uint4(~0u, ~0u, ~0u, ~0u);
+#pragma unroll
+        for (int j = 0; j < kWQPL; ++j) pidm[lane + 64u * j] = 0;
+        npair = 0;
+        wave_sync();
     }
     const uint32_t jn = (npair + 63) >> 6;  // occupied pair slots per lane (uniform)
     wave_sync();
@@ -393,7 +515,7 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
     KeyT pkv[kWPPL];
     uint32_t keptm = 0, ecnt[kWPPL];
 #pragma unroll
-    for (int j = 0; j < kWPPL; ++j) pkv[j] = pkey_d[lane + 64u * j];
+    for (int j = 0; j < kWPPL && j < (int)jn; ++j) pkv[j] = pkey_d[lane + 64u * j];
     if constexpr (!per_pid) {
         // ---- C1: candidates (priority below the pid's threshold) append
         // their pair key to the pid's region
@@ -403,17 +525,19 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
         // round-0 candidate bound: about k + 2 sqrt(k) + 2 expected
         // candidates per pid (~1.5 % of pids need a second round)
         const float e0 = (float)bp.mpc + DPG_E0_C * sqrtf((float)bp.mpc) + DPG_E0_C;
+        uint32_t bq[kWPPL];  // the pid's pre-filter bound: its pairs' priorities are <= it
         {
             uint32_t pv[kWPPL];
 #pragma unroll
-            for (int j = 0; j < kWPPL; ++j) {
+            for (int j = 0; j < kWPPL && j < (int)jn; ++j) {
                 const uint32_t q = (uint32_t)(pkv[j] >> pkb) & (kWCq - 1);
                 sb[j] = pidslot[q];
                 pv[j] = pidv[q];
                 m[j] = pidm[q] & 0xFFFFu;
+                bq[j] = cbnd[q];
             }
 #pragma unroll
-            for (int j = 0; j < kWPPL; ++j) {
+            for (int j = 0; j < kWPPL && j < (int)jn; ++j) {
                 const bool occ = lane + 64u * j < npair;
                 k64[j] = 0;
                 if (occ) keptm |= 1u << j;
@@ -422,16 +546,16 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
                 const uint32_t pk = (uint32_t)(pkv[j] & (KeyT)pkmask);
                 const uint32_t pr = pair_prio_h(pv[j], pk);
                 k64[j] = ((uint64_t)pr << 32) | pk;
-                if (pr < cand_threshold_e(m[j], e0)) candm |= 1u << j;
+                if (pr < cand_threshold_be(m[j], e0, bq[j])) candm |= 1u << j;
             }
             uint32_t pos[kWPPL];
 #pragma unroll
-            for (int j = 0; j < kWPPL; ++j) {
+            for (int j = 0; j < kWPPL && j < (int)jn; ++j) {
                 const uint32_t q = (uint32_t)(pkv[j] >> pkb) & (kWCq - 1);
                 pos[j] = ((candm >> j) & 1u) ? atomicAdd(&pidm[q], 1u << 16) >> 16 : 0u;
             }
 #pragma unroll
-            for (int j = 0; j < kWPPL; ++j)
+            for (int j = 0; j < kWPPL && j < (int)jn; ++j)
                 if ((candm >> j) & 1u) pool[sb[j] + pos[j]] = k64[j];
         }
         wave_sync();
@@ -463,24 +587,25 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
                 wave_sync();
                 uint32_t ncp[kWPPL], pos[kWPPL], newm = 0;
 #pragma unroll
-                for (int j = 0; j < kWPPL; ++j) {
+                for (int j = 0; j < kWPPL && j < (int)jn; ++j) {
                     const uint32_t q = (uint32_t)(pkv[j] >> pkb) & (kWCq - 1);
                     ncp[j] = pidm[q] >> 16;
                 }
 #pragma unroll
-                for (int j = 0; j < kWPPL; ++j) {
+                for (int j = 0; j < kWPPL && j < (int)jn; ++j) {
                     const bool over = (overm >> j) & 1u, cand = (candm >> j) & 1u;
                     if (over && !cand && ncp[j] < bp.mpc &&
-                        (rnd > 0 || (uint32_t)(k64[j] >> 32) < cand_threshold_e(m[j], 4.0f * e0)))
+                        (rnd > 0 ||
+                         (uint32_t)(k64[j] >> 32) < cand_threshold_be(m[j], 4.0f * e0, bq[j])))
                         newm |= 1u << j;
                 }
 #pragma unroll
-                for (int j = 0; j < kWPPL; ++j) {
+                for (int j = 0; j < kWPPL && j < (int)jn; ++j) {
                     const uint32_t q = (uint32_t)(pkv[j] >> pkb) & (kWCq - 1);
                     pos[j] = ((newm >> j) & 1u) ? atomicAdd(&pidm[q], 1u << 16) >> 16 : 0u;
                 }
 #pragma unroll
-                for (int j = 0; j < kWPPL; ++j)
+                for (int j = 0; j < kWPPL && j < (int)jn; ++j)
                     if ((newm >> j) & 1u) pool[sb[j] + pos[j]] = k64[j];
                 candm |= newm;
                 wave_sync();
@@ -490,9 +615,9 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
         {
             uint64_t thr[kWPPL];
 #pragma unroll
-            for (int j = 0; j < kWPPL; ++j) thr[j] = pool[((overm >> j) & 1u) ? sb[j] : 0u];
+            for (int j = 0; j < kWPPL && j < (int)jn; ++j) thr[j] = pool[((overm >> j) & 1u) ? sb[j] : 0u];
 #pragma unroll
-            for (int j = 0; j < kWPPL; ++j) {
+            for (int j = 0; j < kWPPL && j < (int)jn; ++j) {
                 const bool over = (overm >> j) & 1u, cand = (candm >> j) & 1u;
                 if (over && !(cand && k64[j] <= thr[j])) keptm &= ~(1u << j);
             }
@@ -504,10 +629,10 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
         uint32_t c[kWPPL], b2[kWPPL];
         {
 #pragma unroll
-            for (int j = 0; j < kWPPL; ++j) c[j] = pcnt[lane + 64u * j];
+            for (int j = 0; j < kWPPL && j < (int)jn; ++j) c[j] = pcnt[lane + 64u * j];
             uint32_t run = 0;
 #pragma unroll
-            for (int j = 0; j < kWPPL; ++j) {
+            for (int j = 0; j < kWPPL && j < (int)jn; ++j) {
                 const bool need = sample && ((keptm >> j) & 1u) && c[j] > bp.mcpp;
                 uint32_t tot;
                 const uint32_t ex = wave_excl_scan(need ? c[j] : 0u, tot);
@@ -515,7 +640,7 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
                 run += tot;
             }
 #pragma unroll
-            for (int j = 0; j < kWPPL; ++j) {
+            for (int j = 0; j < kWPPL && j < (int)jn; ++j) {
                 if (lane + 64u * j < npair)
                     pst[lane + 64u * j] = ((keptm >> j) & 1u) ? b2[j] : kDropped;
                 ecnt[j] = bp.mode == DPG_MODE_CROSS_AND_PER_PARTITION ? min(c[j], bp.mcpp) : c[j];
@@ -529,31 +654,31 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
         double v[kWRPT];
         uint32_t st[kWRPT];
 #pragma unroll
-        for (int k = 0; k < kWRPT; ++k) st[k] = pst[dn[k]];
+        for (int k = 0; k < kWRPT && k < (int)kn; ++k) st[k] = pst[dn[k]];
 #pragma unroll
-        for (int k = 0; k < kWRPT; ++k) {
-            if (!((validm >> k) & 1u)) st[k] = kDropped;
+        for (int k = 0; k < kWRPT && k < (int)kn; ++k) {
+            if (!((insm >> k) & 1u)) st[k] = kDropped;
             if (st[k] < kKeptAll) st[k] &= 0xFFFFu;  // base (appends in the high bits)
             v[k] = 0.0;
             rkey[k] = 0;
-            if (need_v && st[k] != kDropped) v[k] = bp.value[RecOps<R>::idx(r[k], f)];
+            if (need_v && st[k] != kDropped) v[k] = bp.value[RecOps<R>::idx(cur[k], f)];
         }
         if (sample) {
             uint32_t pv[kWRPT], pos[kWRPT];
 #pragma unroll
-            for (int k = 0; k < kWRPT; ++k) pv[k] = pidv[qs[k]];
+            for (int k = 0; k < kWRPT && k < (int)kn; ++k) pv[k] = pidv[qs[k]];
 #pragma unroll
-            for (int k = 0; k < kWRPT; ++k) {
+            for (int k = 0; k < kWRPT && k < (int)kn; ++k) {
                 if (st[k] >= kKeptAll) continue;
-                const uint64_t key = RecOps<R>::key(r[k], f);
+                const uint64_t key = RecOps<R>::key(cur[k], f);
                 rkey[k] = rec_prio_h(pv[k], (uint32_t)(key & pkmask),
-                                     (uint64_t)(bp.rec_base + RecOps<R>::idx(r[k], f)));
+                                     (uint64_t)(bp.rec_base + RecOps<R>::idx(cur[k], f)));
             }
 #pragma unroll
-            for (int k = 0; k < kWRPT; ++k)
+            for (int k = 0; k < kWRPT && k < (int)kn; ++k)
                 pos[k] = st[k] < kKeptAll ? atomicAdd(&pst[dn[k]], 1u << 16) >> 16 : 0u;
 #pragma unroll
-            for (int k = 0; k < kWRPT; ++k)
+            for (int k = 0; k < kWRPT && k < (int)kn; ++k)
                 if (st[k] < kKeptAll) pool[st[k] + pos[k]] = rkey[k];
             wave_sync();
         }
@@ -563,24 +688,24 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
         if (need_v) {
             uint32_t keepm = 0;
 #pragma unroll
-            for (int k = 0; k < kWRPT; ++k) keepm |= st[k] == kKeptAll ? 1u << k : 0u;
+            for (int k = 0; k < kWRPT && k < (int)kn; ++k) keepm |= st[k] == kKeptAll ? 1u << k : 0u;
             if (sample) {
                 // threshold of every over-full kept pair; a sampled record is
                 // kept iff its key is <= the threshold
                 bool needp[kWPPL];
 #pragma unroll
-                for (int j = 0; j < kWPPL; ++j) needp[j] = b2[j] < kKeptAll;
+                for (int j = 0; j < kWPPL; ++j) needp[j] = j < (int)jn && b2[j] < kKeptAll;
                 region_thresholds<kWPPL>(pool, needp, b2, c, bp.mcpp);
                 wave_sync();
                 uint64_t thr[kWRPT];
 #pragma unroll
-                for (int k = 0; k < kWRPT; ++k) thr[k] = pool[st[k] < kKeptAll ? st[k] : 0u];
+                for (int k = 0; k < kWRPT && k < (int)kn; ++k) thr[k] = pool[st[k] < kKeptAll ? st[k] : 0u];
 #pragma unroll
-                for (int k = 0; k < kWRPT; ++k)
+                for (int k = 0; k < kWRPT && k < (int)kn; ++k)
                     if (st[k] < kKeptAll && rkey[k] <= thr[k]) keepm |= 1u << k;
             }
 #pragma unroll
-            for (int k = 0; k < kWRPT; ++k) {
+            for (int k = 0; k < kWRPT && k < (int)kn; ++k) {
                 if (!((keepm >> k) & 1u)) continue;
                 const uint32_t p = dn[k];
                 if (part_clip) {
@@ -605,24 +730,24 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
         uint64_t rkey[kWRPT];
         uint32_t sb[kWRPT], pv[kWRPT], pos[kWRPT], overm = 0;
 #pragma unroll
-        for (int k = 0; k < kWRPT; ++k) {
+        for (int k = 0; k < kWRPT && k < (int)kn; ++k) {
             sb[k] = pidslot[qs[k]];
             pv[k] = pidv[qs[k]];
         }
 #pragma unroll
-        for (int k = 0; k < kWRPT; ++k) {
+        for (int k = 0; k < kWRPT && k < (int)kn; ++k) {
             rkey[k] = 0;
             if (!((validm >> k) & 1u) || sb[k] == kNil) continue;
             overm |= 1u << k;
-            const uint64_t key = RecOps<R>::key(r[k], f);
+            const uint64_t key = RecOps<R>::key(cur[k], f);
             rkey[k] = rec_prio_h(pv[k], (uint32_t)(key & pkmask),
-                                 (uint64_t)(bp.rec_base + RecOps<R>::idx(r[k], f)));
+                                 (uint64_t)(bp.rec_base + RecOps<R>::idx(cur[k], f)));
         }
 #pragma unroll
-        for (int k = 0; k < kWRPT; ++k)
+        for (int k = 0; k < kWRPT && k < (int)kn; ++k)
             pos[k] = ((overm >> k) & 1u) ? atomicAdd(&pidm[qs[k]], 1u << 16) >> 16 : 0u;
 #pragma unroll
-        for (int k = 0; k < kWRPT; ++k)
+        for (int k = 0; k < kWRPT && k < (int)kn; ++k)
             if ((overm >> k) & 1u) pool[sb[k] + pos[k]] = rkey[k];
         wave_sync();
         mark(bp, 5, clk);
@@ -641,16 +766,16 @@ bool overp[kWQPL];
         wave_sync();
         uint64_t thr[kWRPT];
 #pragma unroll
-        for (int k = 0; k < kWRPT; ++k) thr[k] = pool[((overm >> k) & 1u) ? sb[k] : 0u];
+        for (int k = 0; k < kWRPT && k < (int)kn; ++k) thr[k] = pool[((overm >> k) & 1u) ? sb[k] : 0u];
         double v[kWRPT];
 #pragma unroll
-        for (int k = 0; k < kWRPT; ++k) {
+        for (int k = 0; k < kWRPT && k < (int)kn; ++k) {
             v[k] = 0.0;
             if (((overm >> k) & 1u) && rkey[k] > thr[k]) validm &= ~(1u << k);
-            if (need_v && ((validm >> k) & 1u)) v[k] = bp.value[RecOps<R>::idx(r[k], f)];
+            if (need_v && ((validm >> k) & 1u)) v[k] = bp.value[RecOps<R>::idx(cur[k], f)];
         }
 #pragma unroll
-        for (int k = 0; k < kWRPT; ++k) {
+        for (int k = 0; k < kWRPT && k < (int)kn; ++k) {
             if (!((validm >> k) & 1u)) continue;
             const uint32_t p = dn[k];
             atomicAdd(&pst[p], 1u);
@@ -671,16 +796,16 @@ bool overp[kWQPL];
         wave_sync();
         mark(bp, 7, clk);
 #pragma unroll
-        for (int j = 0; j < kWPPL; ++j) ecnt[j] = pst[lane + 64u * j];
+        for (int j = 0; j < kWPPL && j < (int)jn; ++j) ecnt[j] = pst[lane + 64u * j];
 #pragma unroll
-        for (int j = 0; j < kWPPL; ++j)
+        for (int j = 0; j < kWPPL && j < (int)jn; ++j)
             if (lane + 64u * j < npair && ecnt[j] > 0) keptm |= 1u << j;
     }
     // ---- G: emit kept pairs; clear the key table
     {
         double a0[kWPPL], a1[kWPPL], a2[kWPPL];
 #pragma unroll
-        for (int j = 0; j < kWPPL; ++j) {
+        for (int j = 0; j < kWPPL && j < (int)jn; ++j) {
             const uint32_t d = lane + 64u * j;
             a0[j] = need_v ? acc_sum[d] : 0.0;
             if constexpr (kVar) {
@@ -689,7 +814,7 @@ bool overp[kWQPL];
             }
         }
 #pragma unroll
-        for (int j = 0; j < kWPPL; ++j) {
+        for (int j = 0; j < kWPPL && j < (int)jn; ++j) {
             const bool e = (keptm >> j) & 1u;
             const uint64_t be = __ballot(e);
             if (e) {
@@ -717,7 +842,10 @@ bool overp[kWQPL];
             reinterpret_cast<uint4 *>(keys)[lane + 64u * i] = make_uint4(~0u, ~0u, ~0u, ~0u);
     }
 #pragma unroll
-    for (int j = 0; j < kWQPL; ++j) pidm[qv[j]] = 0;
+    for (int j = 0; j < kWQPL; ++j) {
+        pidm[qv[j]] = 0;
+        pidslot[qv[j]] = 0;
+    }
     wave_sync();
     mark(bp, 8, clk);
     return nitems;
@@ -752,8 +880,9 @@ __global__ __launch_bounds__(64, kWCap <= 384 ? 3 : 2) void k_bound_waves(const 
     const uint32_t lane = __lane_id();
     {
         uint32_t *pidm = reinterpret_cast<uint32_t *>(smem + L::PIDM);
+        uint32_t *pidslot = reinterpret_cast<uint32_t *>(smem + L::PIDSLOT);
         KeyT *keys = reinterpret_cast<KeyT *>(smem + L::KEYS);
-        for (uint32_t i = lane; i < kWCq; i += 64) pidm[i] = 0;
+        for (uint32_t i = lane; i < kWCq; i += 64) pidm[i] = pidslot[i] = 0;
         for (uint32_t i = lane; i < kWCk; i += 64) keys[i] = empty_key<KeyT>();
     }
     wave_sync();

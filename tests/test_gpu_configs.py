@@ -64,7 +64,9 @@ def test_config2_nonbinding_bounds_equal_exact_groupby(built, config2_data):
     input (numpy, independent of the oracle): counts and privacy-id counts
     bit-exact, sums within 1e-9 relative."""
     pid, pk, val = config2_data
-    _, _, got = _run(pid, pk, val, _c2_params(10**6, 10**6), P2, pid_range=(0, U2))
+    # 1000 exceeds every privacy id's pairs and every pair's records here
+    assert np.bincount(pid).max() < 1000
+    _, _, got = _run(pid, pk, val, _c2_params(1000, 1000), P2, pid_range=(0, U2))
     count = np.bincount(pk, minlength=P2)
     s = np.bincount(pk, weights=np.clip(val, 0.0, 10.0), minlength=P2)
     pairs = np.unique(pid * P2 + pk)

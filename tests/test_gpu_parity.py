@@ -297,3 +297,36 @@ def test_gpu_wide_records(built):
     assert np.array_equal(got["rows"], ref["rows"])
     assert np.array_equal(got["count"], ref["count"])
     assert np.allclose(got["sum"], ref["sum"], rtol=1e-9, atol=1e-9)
+
+
+@pytest.mark.parametrize("mpc", [1, 4, 9])
+def test_gpu_candidate_prefilter_and_restart(built, mpc):
+    """The wave kernel inserts only records whose pair priority is below a
+    per-pid bound; a pid left with fewer than mpc candidate pairs restarts
+    the chunk with every record.  Privacy ids here put many records into few
+    partitions (bound far too tight: restarts) or spread them over many
+    (no restart); partials equal the oracle's either way."""
+    rng = np.random.default_rng(90 + mpc)
+    P = 4000
+    n_pid = 6000
+    recs = rng.integers(1, 60, n_pid)                 # records per pid
+    parts = np.where(rng.random(n_pid) < 0.5, rng.integers(1, 4, n_pid),
+                     rng.integers(10, 50, n_pid))     # distinct partitions per pid
+    pid = np.repeat(np.arange(n_pid), recs)
+    base = rng.integers(0, P, n_pid)
+    off = np.concatenate([rng.integers(0, p, r) for p, r in zip(parts, recs)])
+    pk = (np.repeat(base, recs) + off * 37) % P
+    order = rng.permutation(len(pid))
+    pid, pk = pid[order].astype(np.int64), pk[order].astype(np.int64)
+    val = rng.uniform(-1.0, 11.0, len(pid))
+    params = pdp.AggregateParams(metrics=[pdp.Metrics.COUNT, pdp.Metrics.SUM,
+                                          pdp.Metrics.PRIVACY_ID_COUNT],
+                                 max_partitions_contributed=mpc, max_contributions_per_partition=2,
+                                 min_value=0.0, max_value=10.0)
+    res, _ = run_engine(pid, pk, val, params, public=list(range(P)), n_partitions=P)
+    ref = oracle.bound_aggregate(pid, pk, val, res.last_bound_fields, SEED,
+                                 public_mask=oracle.bitmap(range(P), P))
+    got = {k: v.cpu().numpy() for k, v in res.last_partials.items() if v is not None}
+    assert np.array_equal(got["rows"], ref["rows"])
+    assert np.array_equal(got["count"], ref["count"])
+    assert np.allclose(got["sum"], ref["sum"], rtol=1e-9, atol=1e-9)
