@@ -442,8 +442,9 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     if (timing) {
         unsigned long long h[32];
         HIP_TRY(hipMemcpy(h, bpl.phase_cyc, sizeof(h), hipMemcpyDeviceToHost));
-        static const char *nmw[10] = {"A0.cas", "A1.count", "B.slots", "C1.cand", "C2.rank",
-                                      "D.state", "E.mcpp", "F.acc", "G.emit", "A.probe"};
+        static const char *nmw[12] = {"A0.cas", "A1.count", "B.slots", "C1.cand", "C2.rank",
+                                      "D.state", "E.mcpp", "F.acc", "G.emit", "A.probe",
+                                      "Am.pidc", "Am.cand"};
         static const char *nmc[9] = {"A0.cas", "A1.count", "A2.barrier", "B.slots", "C.mpc",
                                      "D.state", "E.mcpp", "F.acc", "G.emit"};
         for (int part = 0; part < 2; ++part) {
@@ -451,7 +452,7 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
             const uint32_t gg = part ? Gm : Gw;
             if (!gg) continue;
             unsigned long long tot = 0;
-            const int np = part ? 9 : 10;
+            const int np = part ? 9 : 12;
             for (int i = 0; i < np; ++i) tot += hp[i];
             std::fprintf(stderr, "[dpg phase] %s chunks=%u over=%u over2=%u per-WG Mcycles:",
                          part ? "medium" : "small", part ? hctl.n_mchunks : hctl.n_chunks,

@@ -62,7 +62,7 @@ __device__ __forceinline__ uint64_t pid_of(const BoundParams &bp, uint32_t d1, u
 #ifdef DPG_PHASE_TIMING
 struct PhaseTimer {
     uint64_t last;
-    uint64_t pt[10];
+    uint64_t pt[12];
 };
 #else
 struct PhaseTimer {};
@@ -85,7 +85,7 @@ __device__ __forceinline__ void mark(const BoundParams &bp, uint32_t phase, Phas
 __device__ __forceinline__ void timer_start(const BoundParams &bp, PhaseTimer &tm) {
 #ifdef DPG_PHASE_TIMING
     tm.last = bp.phase_cyc ? __builtin_amdgcn_s_memtime() : 0;
-    for (int k = 0; k < 10; ++k) tm.pt[k] = 0;
+    for (int k = 0; k < 12; ++k) tm.pt[k] = 0;
 #else
     (void)bp;
     (void)tm;
@@ -94,7 +94,7 @@ __device__ __forceinline__ void timer_start(const BoundParams &bp, PhaseTimer &t
 __device__ __forceinline__ void timer_flush(const BoundParams &bp, const PhaseTimer &tm) {
 #ifdef DPG_PHASE_TIMING
     if (bp.phase_cyc && threadIdx.x == 0)
-        for (int k = 0; k < 10; ++k) atomicAdd(&bp.phase_cyc[k], (unsigned long long)tm.pt[k]);
+        for (int k = 0; k < 12; ++k) atomicAdd(&bp.phase_cyc[k], (unsigned long long)tm.pt[k]);
 #else
     (void)bp;
     (void)tm;

@@ -287,6 +287,7 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
         }
     }
     wave_sync();
+    mark(bp, 10, clk);
     if constexpr (!kPerPid) {
         uint32_t pv[kWRPT], cb[kWRPT];
 #pragma unroll
@@ -302,6 +303,7 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
     } else {
         insm = validm;
     }
+    mark(bp, 11, clk);
     // the candidates, compacted into the first slots (pool + accumulator
     // area: idle until phase A), are the records the phases below work on;
     // a restart switches back to all of them
