@@ -53,6 +53,8 @@ struct Control {  // device-side counters, zeroed per call
     uint32_t n_over;   // fine buckets over the chunk capacity
     uint32_t n_over2;  // refined buckets still over it
     uint32_t n_mchunks;  // single-bucket chunks above the small-chunk capacity
+    uint32_t heavy_nfb;  // heavy buckets handed back to k_bound_big
+    uint32_t pad_;
     unsigned long long over_records;
     unsigned long long over2_records;
     unsigned long long pid_lo, pid_hi;  // order-preserving (x ^ 2^63) min / max
@@ -311,7 +313,7 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     if (hctl.err & 1u)
         return fail(ctx, DPG_ERR_KEY_RANGE,
                     "privacy id outside its declared range or partition key outside [0, P)");
-    const uint4 *chunk_list = chunks;
+    uint4 *chunk_list = chunks;
     const uint4 *mchunk_list = mchunks;
     const R *refined = recs;
     // global-memory leftovers: (buffer, starts, counts, level-1 buckets, number)
@@ -375,6 +377,28 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
             n_global = hctl.n_over2;
         }
     }
+    // ---- heavy buckets (single privacy ids over every chunk, cross-partition
+    // modes): candidate records into heavy chunks of the small-chunk list
+    // (dpg_wave.h); the rest, and buckets the wave kernel hands back, stay on
+    // the global-memory path.  mpc <= 128: ~mpc pairs below a 512-record cut.
+    const bool per_pid = bp.mode == DPG_MODE_PER_PRIVACY_ID;
+    const bool heavy = n_global > 0 && !per_pid && !ItemTraits<Item>::preagg && bp.mpc <= 128 &&
+                       std::getenv("DPG_NO_HEAVY") == nullptr;
+    const R *hrec = recs;
+    uint32_t *hfb = nullptr;
+    if (heavy) {
+        stage(ctx, s, "heavy");
+        WS(hr, R, "heavy.recs", (size_t)n_global * kWCap);
+        WS(hf, uint32_t, "heavy.fb", n_global);
+        BoundParams bph = bp;
+        bph.heavy_fb = hf;
+        bph.heavy_nfb = &ctl->heavy_nfb;
+        k_heavy_filter<R><<<n_global, kHvThreads, 0, s>>>(g_base, g_start, g_cnt, g_d1, bph, hr,
+                                                          chunk_list, &ctl->n_chunks);
+        LAUNCH_CHECK();
+        hrec = hr;
+        hfb = hf;
+    }
     // ---- bounding in LDS: Gw single-wave workgroups over the small chunks,
     // Gm 256-thread workgroups over the medium ones (launched only if there
     // are any), the global-memory path last; workgroup g of the Gw + Gm + 1
@@ -383,7 +407,6 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     // file, whichever binds (a static schedule must not oversubscribe)
     // one kernel per bounding family (PER_PRIVACY_ID or cross-partition), so
     // that the hot one holds one path only
-    const bool per_pid = bp.mode == DPG_MODE_PER_PRIVACY_ID;
     auto wave_kern = per_pid ? k_bound_waves<KeyT, Item, R, true> : k_bound_waves<KeyT, Item, R, false>;
     int wpc = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&wpc, wave_kern, 64, WL::TOTAL) != hipSuccess ||
@@ -394,7 +417,8 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
                                              ctx->n_cu * CL::PER_CU, hctl.n_mchunks)
                                        : 0u;
     const uint32_t G = Gw + Gm;
-    WS(items, Item, "items", std::max<int64_t>(n, 1));
+    // heavy buckets handed back are counted twice (candidates + bucket)
+    WS(items, Item, "items", std::max<int64_t>(n + (heavy ? (int64_t)n_global * kWCap : 0), 1));
     WS(wg_rec, uint32_t, "wg.rec", G + 1);
     WS(wg_off, int64_t, "wg.off", G + 2);
     WS(wg_cnt, uint32_t, "wg.cnt", G + 1);
@@ -413,6 +437,8 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     bpl.progress = prog;
     const bool timing = std::getenv("DPG_PHASE_TIMING") != nullptr;
     bpl.phase_cyc = nullptr;
+    bpl.heavy_fb = hfb;
+    bpl.heavy_nfb = &ctl->heavy_nfb;
     if (timing) {
         WS(pc, unsigned long long, "bound.phase_cyc", 48);
         HIP_TRY(hipMemsetAsync(pc, 0, 48 * 8, s));
@@ -421,7 +447,7 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     (void)hipFuncSetAttribute((const void *)wave_kern,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)WL::TOTAL);
     stage(ctx, s, "bound");
-    wave_kern<<<Gw, 64, WL::TOTAL, s>>>(recs, refined, chunk_list,
+    wave_kern<<<Gw, 64, WL::TOTAL, s>>>(recs, refined, hrec, chunk_list,
                                                           &ctl->n_chunks, bpl, items, wg_off,
                                                           wg_cnt);
     LAUNCH_CHECK();
@@ -464,6 +490,24 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
         }
     }
     // ---- single buckets beyond the chunk capacity: global-memory working sets
+    if (heavy) {
+        HIP_TRY(hipMemcpyAsync(&hctl, ctl, sizeof(Control), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        const uint32_t nfb = hctl.heavy_nfb;
+        if (nfb > 0) {
+            WS(fst, int64_t, "heavy.fb.start", nfb);
+            WS(fcnt, uint32_t, "heavy.fb.cnt", nfb);
+            WS(fd1, uint32_t, "heavy.fb.d1", nfb);
+            k_gather_heavy<<<(nfb + 255) / 256, 256, 0, s>>>(hfb, &ctl->heavy_nfb, g_start, g_cnt,
+                                                             g_d1, fst, fcnt, fd1);
+            LAUNCH_CHECK();
+            g_start = fst;
+            g_cnt = fcnt;
+            g_d1 = fd1;
+        }
+        if (timing) std::fprintf(stderr, "[dpg phase] heavy buckets=%u handed back=%u\n", n_global, nfb);
+        n_global = nfb;
+    }
     if (n_global > 0) {
         std::vector<uint32_t> cnt(n_global);
         HIP_TRY(hipMemcpy(cnt.data(), g_cnt, n_global * 4, hipMemcpyDeviceToHost));

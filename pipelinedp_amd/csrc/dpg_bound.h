@@ -45,6 +45,8 @@ struct BoundParams {
     uint32_t *err;         // bit 1: internal table error
     uint32_t *progress;    // debug watchdog: last phase per workgroup (or null)
     unsigned long long *phase_cyc;  // debug: shader cycles per phase (or null)
+    uint32_t *heavy_fb;    // heavy buckets handed back to k_bound_big (indices)
+    uint32_t *heavy_nfb;   // their number
 };
 
 // privacy id of a bucket's pid-hash residual

@@ -547,8 +547,12 @@ __device__ __forceinline__ void bound_chunk(const R (&r)[kRPT], uint32_t n, uint
     mark(bp, 8, clk);
 }
 
-// Chunk descriptor: records [x, x + (y & 0x7FFFFFFF)) of buffer (y >> 31),
-// level-1 bucket z, pid hash-residual base w.
+// Chunk descriptor: records [x, x + (y & kChunkCount)) of buffer (y >> 31),
+// level-1 bucket z, pid hash-residual base w.  Heavy chunks (bit 30 of y,
+// small-chunk list only, dpg_wave.h) hold the candidate records of one heavy
+// privacy id in their own buffer, with the candidate cut in z >> 16.
+constexpr uint32_t kChunkCount = 0x3FFFFFFFu;
+constexpr uint32_t kChunkHeavy = 0x40000000u;
 template <class R>
 __device__ __forceinline__ const R *chunk_base(uint4 d, const R *b0, const R *b1) {
     return ((d.y >> 31) ? b1 : b0) + d.x;
@@ -625,7 +629,7 @@ __global__ __launch_bounds__(256) void k_wg_records(const uint4 *chunks, const u
     __shared__ uint32_t part[4];
     const uint32_t nch = *n_chunks, g = blockIdx.x;
     uint32_t acc = 0;
-    for (uint32_t w = g + threadIdx.x * G; w < nch; w += 256 * G) acc += chunks[w].y & 0x7FFFFFFFu;
+    for (uint32_t w = g + threadIdx.x * G; w < nch; w += 256 * G) acc += chunks[w].y & kChunkCount;
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
     if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
     __syncthreads();

@@ -79,6 +79,21 @@ struct WaveLayout {
 #define DPG_CAND_C 2.0f
 #endif
 
+// Heavy chunks (k_heavy_filter): the candidate records of one privacy id
+// whose bucket exceeds every LDS chunk, in their own buffer, kWCap slots per
+// heavy bucket; the candidate bound is (cut << 20) - 1 with cut = z >> 16.
+constexpr uint32_t kHvBins = 4096;  // cut granularity: 2^20 of the 2^32 priority range
+__device__ __forceinline__ uint32_t heavy_bound(uint4 d) {
+    if (!(d.y & kChunkHeavy)) return 0u;
+    const uint32_t cut = d.z >> 16;
+    return cut >= kHvBins ? 0xFFFFFFFFu : (cut << 20) - 1u;
+}
+template <class R>
+__device__ __forceinline__ const R *wave_chunk_base(uint4 d, const R *recs, const R *refined,
+                                                    const R *heavy) {
+    return ((d.y & kChunkHeavy) ? heavy : (d.y >> 31) ? refined : recs) + d.x;
+}
+
 // Compiler-level ordering of one wave's LDS accesses between phases (the
 // hardware already executes them in order).
 __device__ __forceinline__ void wave_sync() {
@@ -196,7 +211,8 @@ __device__ __forceinline__ void region_thresholds(uint64_t *pool, const bool (&s
 template <class KeyT, class Item, class R, bool kPerPid>
 __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, uint32_t d1,
                                                uint32_t hbase, char *smem, const BoundParams &bp,
-                                               Item *items, uint32_t nitems, PhaseTimer &clk) {
+                                               Item *items, uint32_t nitems, PhaseTimer &clk,
+                                               uint32_t hbound = 0, uint32_t hidx = 0) {
     using L = WaveLayout<KeyT, Item>;
     constexpr bool kVar = L::var;
     uint32_t *pidv = reinterpret_cast<uint32_t *>(smem + L::PIDV);
@@ -272,8 +288,11 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
                                                            (d1 << hshift) | (hbase + q), bp.hash)));
                 const uint32_t rc = pidslot[q];
                 const float fr = cmul / (float)rc;
-                cbnd[q] = rc <= bp.mpc || fr >= 1.0f ? 0xFFFFFFFFu
-                                                     : (uint32_t)(fr * 4294967296.0f);
+                // a heavy chunk holds the candidates of one pid, filtered by
+                // k_heavy_filter with the bound hbound
+                cbnd[q] = hbound ? hbound
+                                 : (rc <= bp.mpc || fr >= 1.0f ? 0xFFFFFFFFu
+                                                               : (uint32_t)(fr * 4294967296.0f));
             }
         }
     } else {
@@ -485,6 +504,15 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
 #pragma unroll
         for (int j = 0; j < kWQPL; ++j) pidm[lane + 64u * j] = 0;
         npair = 0;
+        if (hbound) {
+            // a heavy chunk holds only its pid's candidates: the bucket goes
+            // back to the global-memory kernel (rare)
+#pragma unroll
+            for (int j = 0; j < kWQPL; ++j) pidslot[lane + 64u * j] = 0;
+            if (lane == 0) bp.heavy_fb[atomicAdd(bp.heavy_nfb, 1u)] = hidx;
+            wave_sync();
+            return nitems;
+        }
         wave_sync();
     }
     const uint32_t jn = (npair + 63) >> 6;  // occupied pair slots per lane (uniform)
@@ -858,7 +886,8 @@ bool overp[kWQPL];
 // and leaves the count in wg_cnt[g].
 template <class KeyT, class Item, class R, bool kPerPid>
 __global__ __launch_bounds__(64, kWCap <= 384 ? 3 : 2) void k_bound_waves(const R *recs, const R *refined,
-                                                    const uint4 *chunks, const uint32_t *n_chunks,
+                                                    const R *heavy, const uint4 *chunks,
+                                                    const uint32_t *n_chunks,
                                                     BoundParams bp, Item *items,
                                                     const int64_t *wg_off, uint32_t *wg_cnt) {
     using L = WaveLayout<KeyT, Item>;
@@ -891,14 +920,19 @@ __global__ __launch_bounds__(64, kWCap <= 384 ? 3 : 2) void k_bound_waves(const 
     R r[kWRPT], rn[kWRPT];
     const uint32_t G = gridDim.x;
     uint32_t w = blockIdx.x;
-    uint32_t n = 0, d1 = 0, hb = 0, nitems = 0;
+    uint32_t n = 0, d1 = 0, hb = 0, hbound = 0, hidx = 0, nitems = 0;
     uint4 dn = make_uint4(0, 0, 0, 0);
     if (w < nch) {
-        const uint4 d = chunks[w];
-        n = __builtin_amdgcn_readfirstlane(d.y & 0x7FFFFFFFu);
-        d1 = __builtin_amdgcn_readfirstlane(d.z);
-        hb = __builtin_amdgcn_readfirstlane(d.w);
-        const R *b = chunk_base(d, recs, refined);
+        const uint4 d = make_uint4(__builtin_amdgcn_readfirstlane(chunks[w].x),
+                                   __builtin_amdgcn_readfirstlane(chunks[w].y),
+                                   __builtin_amdgcn_readfirstlane(chunks[w].z),
+                                   __builtin_amdgcn_readfirstlane(chunks[w].w));
+        n = d.y & kChunkCount;
+        d1 = d.z & 0xFFFFu;
+        hb = d.w;
+        hbound = heavy_bound(d);
+        hidx = d.x / (uint32_t)kWCap;
+        const R *b = wave_chunk_base(d, recs, refined, heavy);
 #pragma unroll
         for (int k = 0; k < kWRPT; ++k) r[k] = b[min(lane + 64u * k, n - 1)];
         if (w + G < nch) dn = chunks[w + G];
@@ -910,23 +944,132 @@ __global__ __launch_bounds__(64, kWCap <= 384 ? 3 : 2) void k_bound_waves(const 
                                     __builtin_amdgcn_readfirstlane(dn.y),
                                     __builtin_amdgcn_readfirstlane(dn.z),
                                     __builtin_amdgcn_readfirstlane(dn.w));
-        const uint32_t nn = du.y & 0x7FFFFFFFu;
+        const uint32_t nn = du.y & kChunkCount;
         // the next chunk's records load while this one is processed
         if (nn > 0) {
-            const R *nb = chunk_base(du, recs, refined);
+            const R *nb = wave_chunk_base(du, recs, refined, heavy);
 #pragma unroll
             for (int k = 0; k < kWRPT; ++k) rn[k] = nb[min(lane + 64u * k, nn - 1)];
         }
-        nitems = wave_chunk<KeyT, Item, R, kPerPid>(r, n, d1, hb, smem, bp, my_items, nitems, clk);
+        nitems = wave_chunk<KeyT, Item, R, kPerPid>(r, n, d1, hb, smem, bp, my_items, nitems, clk,
+                                                    hbound, hidx);
 #pragma unroll
         for (int k = 0; k < kWRPT; ++k) r[k] = rn[k];
         n = nn;
-        d1 = du.z;
+        d1 = du.z & 0xFFFFu;
         hb = du.w;
+        hbound = heavy_bound(du);
+        hidx = du.x / (uint32_t)kWCap;
         dn = dnn;
     }
     if (lane == 0) wg_cnt[blockIdx.x] = nitems;
     timer_flush(bp, clk);
+}
+
+// Heavy buckets (cross-partition modes): a single privacy id with more
+// records than any LDS chunk holds (config 4's Pareto tail: 1e5 ids with up
+// to ~2e4 records each).  Only pairs of low priority can be among its mpc
+// kept pairs, and a pair's records share its priority, so one workgroup per
+// bucket histograms the records' pair priorities (4096 bins), picks the
+// largest bin cut with <= kWCap records below it and writes those records --
+// every record of every pair below the cut -- to a heavy chunk that the wave
+// kernel bounds like any other, with the cut as the pid's candidate bound.
+// When fewer than mpc pairs lie below the cut (many records per pair) the
+// wave kernel hands the bucket back to k_bound_big (heavy_fb), as does this
+// kernel for a bucket of several privacy ids.  Two reads of the bucket's
+// records (the second mostly from L2), no global atomics but one per bucket.
+constexpr int kHvThreads = 256;
+template <class R>
+__global__ __launch_bounds__(kHvThreads) void k_heavy_filter(
+    const R *base, const int64_t *bstart, const uint32_t *bcnt, const uint32_t *bd1,
+    BoundParams bp, R *hrec, uint4 *chunks, uint32_t *n_chunks) {
+    __shared__ uint32_t hist[kHvBins];
+    __shared__ uint32_t wtot[kHvThreads / 64];
+    __shared__ uint32_t sh_le, sh_n;
+    const uint32_t b = blockIdx.x;
+    const uint32_t tid = threadIdx.x, lane = __lane_id(), wid = tid >> 6;
+    const uint32_t n = bcnt[b];
+    const uint32_t d1 = bd1[b];
+    const R *rb = base + bstart[b];
+    const Fmt f = bp.fmt;
+    const uint32_t pkb = f.pkbits;
+    const uint64_t pkmask = (1ull << pkb) - 1ull;
+    const uint32_t hres = (uint32_t)(RecOps<R>::key(rb[0], f) >> pkb);
+    const uint32_t pv = pid_hash(bp.seed, pid_of(bp, d1, hres));
+    for (uint32_t i = tid; i < kHvBins; i += kHvThreads) hist[i] = 0;
+    if (tid == 0) sh_le = sh_n = 0;
+    __syncthreads();
+    bool multi = false;
+    for (uint32_t i = tid; i < n; i += kHvThreads) {
+        const uint64_t key = RecOps<R>::key(rb[i], f);
+        multi |= (uint32_t)(key >> pkb) != hres;
+        atomicAdd(&hist[pair_prio_h(pv, (uint32_t)(key & pkmask)) >> 20], 1u);
+    }
+    if (__syncthreads_or(multi)) {
+        if (tid == 0) bp.heavy_fb[atomicAdd(bp.heavy_nfb, 1u)] = b;
+        return;
+    }
+    // cut = max{c : records in bins [0, c) <= kWCap}: cum(c) is
+    // non-decreasing, so the cut is the number of c in [1, 4096] that qualify
+    constexpr uint32_t kPer = kHvBins / kHvThreads;
+    uint32_t s = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; ++j) s += hist[tid * kPer + j];
+    uint32_t tot;
+    uint32_t run = wave_excl_scan(s, tot);
+    if (lane == 0) wtot[wid] = tot;
+    __syncthreads();
+    for (uint32_t w = 0; w < wid; ++w) run += wtot[w];
+    uint32_t le = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; ++j) {
+        run += hist[tid * kPer + j];
+        le += run <= (uint32_t)kWCap ? 1u : 0u;
+    }
+    atomicAdd(&sh_le, le);
+    __syncthreads();
+    const uint32_t cut = sh_le;
+    const uint32_t B = cut >= kHvBins ? 0xFFFFFFFFu : cut ? (cut << 20) - 1u : 0u;
+    R *out = hrec + (size_t)b * kWCap;
+    if (cut) {
+        for (uint32_t i0 = 0; i0 < n; i0 += kHvThreads) {
+            const uint32_t i = i0 + tid;
+            bool c = false;
+            R rec{};
+            if (i < n) {
+                rec = rb[i];
+                c = pair_prio_h(pv, (uint32_t)(RecOps<R>::key(rec, f) & pkmask)) <= B;
+            }
+            const uint64_t bal = __ballot(c);
+            uint32_t o = 0;
+            if (bal) {
+                if (lane == 0) o = atomicAdd(&sh_n, (uint32_t)__popcll(bal));
+                o = __shfl(o, 0, 64);
+            }
+            if (c) out[o + lanes_below(bal)] = rec;
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        const uint32_t cnt = sh_n;
+        if (cnt == 0)
+            bp.heavy_fb[atomicAdd(bp.heavy_nfb, 1u)] = b;
+        else
+            chunks[atomicAdd(n_chunks, 1u)] =
+                make_uint4(b * (uint32_t)kWCap, cnt | kChunkHeavy, d1 | (cut << 16), hres);
+    }
+}
+
+// The buckets handed back (heavy_fb) as an oversize list for k_bound_big.
+__global__ void k_gather_heavy(const uint32_t *fb, const uint32_t *nfb, const int64_t *st,
+                               const uint32_t *cnt, const uint32_t *d1, int64_t *ost,
+                               uint32_t *ocnt, uint32_t *od1) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= *nfb) return;
+    const uint32_t b = fb[i];
+    ost[i] = st[b];
+    ocnt[i] = cnt[b];
+    od1[i] = d1[b];
 }
 
 }  // namespace dpg
