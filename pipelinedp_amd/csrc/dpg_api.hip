@@ -736,7 +736,8 @@ int aggregate_impl(dpg_ctx *ctx, const int64_t *pid, const int64_t *pk, const do
     pl.P = P;
     pl.kbits = std::max<uint32_t>(1, bits_for(U));
     pl.pkbits = std::max<uint32_t>(1, bits_for((uint64_t)P));
-    const uint32_t target = ctx->bucket_target ? ctx->bucket_target : kBucketTarget;
+    uint32_t target = ctx->bucket_target ? ctx->bucket_target : kBucketTarget;
+    if (const char *e = std::getenv("DPG_DEBUG_TARGET")) target = (uint32_t)std::max(1, std::atoi(e));
     // at most 7 pid hash bits may stay below a fine bucket (direct pid slots
     // of a small chunk: kWCq = 128), hence the lower bound kbits - 7
     uint32_t bits_total = bits_for((uint64_t)((n + target - 1) / target));
@@ -747,6 +748,13 @@ int aggregate_impl(dpg_ctx *ctx, const int64_t *pid, const int64_t *pk, const do
     // 16 B per record, so its runs should be the longer ones)
     pl.b1 = bits_total <= kMaxB1 ? bits_total : bits_total / 2;
     pl.b2 = bits_total - pl.b1;
+    if (const char *e = std::getenv("DPG_DEBUG_B1")) {  // debug: level split experiments
+        const uint32_t b1 = (uint32_t)std::atoi(e);
+        if (b1 >= 1 && b1 <= kMaxB1 && b1 <= bits_total && bits_total - b1 <= kMaxB2) {
+            pl.b1 = b1;
+            pl.b2 = bits_total - b1;
+        }
+    }
     pl.plb = pl.kbits - bits_total;
     const uint32_t ib = std::max<uint32_t>(1, bits_for((uint64_t)n));
     const bool r8 = (pl.kbits - pl.b1) + pl.pkbits + ib <= 64;

@@ -120,6 +120,37 @@ __device__ __forceinline__ void region_thresholds_wide(uint64_t *pool, uint64_t 
         mask &= mask - 1;
         const uint32_t sb = __builtin_amdgcn_readlane(vb, l);
         const uint32_t nc = __builtin_amdgcn_readlane(vc, l);
+        if (nc <= 128) {
+            // two entries per lane, one pass over the region's keys (mpc ~ 50:
+            // k + 2 sqrt(k) + 2 candidates just above one wave)
+            const uint64_t x0 = pool[sb + min(lane, nc - 1)];
+            const uint64_t x1 = pool[sb + min(lane + 64u, nc - 1)];
+            uint32_t r0 = 0, r1 = 0;
+            for (uint32_t t = 0; t < nc; t += 8) {
+                uint64_t y[8];
+#pragma unroll
+                for (int w = 0; w < 8; ++w) y[w] = pool[sb + min(t + w, nc - 1)];
+#pragma unroll
+                for (int w = 0; w < 8; ++w) {
+                    const bool in = t + w < nc;
+                    r0 += (in && y[w] < x0) ? 1u : 0u;
+                    r1 += (in && y[w] < x1) ? 1u : 0u;
+                }
+            }
+            // keys are distinct: exactly one entry has rank K - 1
+            const uint64_t b0 = __ballot(r0 == K - 1 && lane < nc);
+            const uint64_t b1 = __ballot(r1 == K - 1 && lane + 64u < nc);
+            if (b0 | b1) {
+                const int m = __builtin_ctzll(b0 ? b0 : b1);
+                const uint64_t x = b0 ? x0 : x1;
+                const uint64_t T = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(x >> 32), m) << 32) |
+                                   __builtin_amdgcn_readlane((uint32_t)x, m);
+                if (lane == 0) pool[sb] = T;
+            } else if (lane == 0) {
+                pool[sb] = ~0ull;
+            }
+            continue;
+        }
         uint64_t T = ~0ull;
         for (uint32_t l0 = 0; l0 < nc; l0 += 64) {
             const uint32_t e = l0 + lane;

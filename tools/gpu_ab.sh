@@ -16,7 +16,7 @@ python3 - <<'PY'
 import glob, json, os
 for f in sorted(glob.glob("gpurun_out/ab_*.json")):
     d = json.load(open(f))
-    st = d["stage_ms"]
+    st = d.get("stage_ms") or {k: v["ms"] for k, v in d["kernels"].items()}
     print(os.path.basename(f)[3:-5], round(d["ms_per_step"], 2),
           {k: round(st.get(k, 0), 2) for k in ("partition1:hist", "partition1:scatter", "partition2:hist",
                                                "partition2:scatter", "bound")})
