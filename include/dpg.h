@@ -29,6 +29,12 @@
  *        (PartitionSelection / Sum / Count / PrivacyIdCount / RawStatistics)
  *        with analysis/poisson_binomial.py:39-83, driven by
  *        analysis/utility_analysis_engine.py:98-143.
+ *   dpg_dataset_histograms <- pipeline_dp/dataset_histograms/
+ *        computing_histograms.py:420-474 (compute_dataset_histograms, over
+ *        the dpg_preaggregate pairs) and :642-684
+ *        (compute_dataset_histograms_on_preaggregated_data), which feed
+ *        DPEngine.calculate_private_contribution_bounds (dp_engine.py:432-484)
+ *        and analysis/parameter_tuning.py:278-348 (tune).
  */
 #ifndef DPG_H_
 #define DPG_H_
@@ -184,7 +190,8 @@ typedef struct dpg_pair_entry {
     double sum;
     uint32_t n_partitions;
     uint32_t n_contributions;
-    uint32_t reserved[2];
+    uint32_t leader;       /* dpg_preaggregate: 1 on one pair per privacy id */
+    uint32_t reserved;
 } dpg_pair_entry;
 
 /* One row of a MultiParameterConfiguration (analysis/data_structures.py
@@ -216,6 +223,30 @@ typedef struct dpg_ua_params {
                                     partitions_sampling_prob, or NULL       */
     const uint8_t *public_mask;  /* device bitmap of public partitions     */
 } dpg_ua_params;
+
+/* Dataset histograms (pipeline_dp/dataset_histograms/histograms.py:60-75).
+ * Integer histograms (L0, L1, LINF, COUNT_PER_PARTITION,
+ * PRIVACY_ID_PER_PARTITION, in this order) have DPG_HIST_INT_BINS bins of 3
+ * significant digits: bin v for v < 1000 ([v, v+1)), else
+ * 1000 + 900 e + (m - 100) for [m 10^(e+1), (m+1) 10^(e+1)), m in [100, 999].
+ * LINF_SUM has DPG_HIST_SUM_BINS equal bins between the smallest and the
+ * largest pair sum; lowers[i] = np.linspace(min, max, bins + 1)[i]. */
+#define DPG_HIST_INT_BINS 16300
+#define DPG_HIST_SUM_BINS 10000
+#define DPG_HIST_L0 0
+#define DPG_HIST_L1 1
+#define DPG_HIST_LINF 2
+#define DPG_HIST_COUNT_PER_PARTITION 3
+#define DPG_HIST_PRIVACY_ID_PER_PARTITION 4
+
+typedef struct dpg_hist_out {
+    uint64_t *int_bins;  /* device [5][DPG_HIST_INT_BINS][3]: count, sum, max;
+                            a bin exists iff count > 0 or max > 0            */
+    uint64_t *sum_count; /* device [DPG_HIST_SUM_BINS] LINF_SUM counts       */
+    double *sum_sum;     /* device [DPG_HIST_SUM_BINS] LINF_SUM sums         */
+    double *sum_max;     /* device [DPG_HIST_SUM_BINS] LINF_SUM maxima       */
+    double *lowers;      /* device [DPG_HIST_SUM_BINS + 1] LINF_SUM lowers   */
+} dpg_hist_out;
 
 typedef struct dpg_ctx dpg_ctx;
 
@@ -305,6 +336,18 @@ int dpg_utility_analysis(dpg_ctx *ctx, const dpg_pair_entry *pairs,
                          const int64_t *partition_start, int64_t n_partitions,
                          const dpg_ua_params *params, double *raw, double *errors, double *keep,
                          double *report, int64_t *n_out, void *stream);
+
+/* Dataset histograms over a pre-aggregate sorted by partition key (pairs,
+ * partition_start as dpg_preaggregate writes them).  pre_aggregated = 0:
+ * the pairs come from dpg_preaggregate, whose pad0 marks one pair per privacy
+ * id (the per-privacy-id histograms count those); 1: user-supplied
+ * (count, sum, n_partitions, n_contributions) rows, L0 / L1 weighted by
+ * 1 / n_partitions per exact value and rounded half to even
+ * (computing_histograms.py:81-102, 482-529).  All outputs are device
+ * arrays, zero-filled by the call. */
+int dpg_dataset_histograms(dpg_ctx *ctx, const dpg_pair_entry *pairs, int64_t n_pairs,
+                           const int64_t *partition_start, int64_t n_partitions,
+                           int32_t pre_aggregated, const dpg_hist_out *out, void *stream);
 
 /* Timing/profiling aid: per-stage device time (ms) of the last
  * dpg_bound_aggregate call, measured with HIP events on its stream.

@@ -7,6 +7,7 @@ backend) and `ColumnarData` (columnar input).  Device compute lives in the
 HIP library pipelinedp_amd/lib/libdpg.so (C ABI: include/dpg.h).
 """
 from pipelinedp_amd.aggregate_params import AggregateParams
+from pipelinedp_amd.aggregate_params import CalculatePrivateContributionBoundsParams
 from pipelinedp_amd.aggregate_params import CountParams
 from pipelinedp_amd.aggregate_params import MechanismType
 from pipelinedp_amd.aggregate_params import Metric
@@ -15,6 +16,7 @@ from pipelinedp_amd.aggregate_params import NoiseKind
 from pipelinedp_amd.aggregate_params import NormKind
 from pipelinedp_amd.aggregate_params import PartitionSelectionStrategy
 from pipelinedp_amd.aggregate_params import PrivacyIdCountParams
+from pipelinedp_amd.aggregate_params import PrivateContributionBounds
 from pipelinedp_amd.aggregate_params import SelectPartitionsParams
 from pipelinedp_amd.aggregate_params import SumParams
 from pipelinedp_amd.budget_accounting import BudgetAccountant
@@ -30,5 +32,6 @@ from pipelinedp_amd.pipeline_backend import MI355XBackend
 from pipelinedp_amd.pipeline_backend import PipelineBackend
 from pipelinedp_amd.pipeline_backend import register_annotator
 from pipelinedp_amd.report_generator import ExplainComputationReport
+from pipelinedp_amd import dataset_histograms
 
 __version__ = "0.1.0"

@@ -18,7 +18,10 @@ EXPORTED = ("dpg_ctx_create", "dpg_ctx_destroy", "dpg_last_error", "dpg_set_seed
             "dpg_set_tuning",
             "dpg_bound_aggregate", "dpg_select_and_noise", "dpg_compact_kept",
             "dpg_last_stage_times", "dpg_stream_seed", "dpg_preaggregate",
-            "dpg_utility_analysis")
+            "dpg_utility_analysis", "dpg_dataset_histograms")
+
+HIST_INT_BINS = 16300  # DPG_HIST_INT_BINS
+HIST_SUM_BINS = 10000  # DPG_HIST_SUM_BINS
 
 
 class BoundParams(ctypes.Structure):
@@ -63,7 +66,14 @@ class PairEntry(ctypes.Structure):
     """dpg_pair_entry: one (privacy id, partition) pair of the pre-aggregate."""
     _fields_ = [("pk", ctypes.c_uint32), ("count", ctypes.c_uint32), ("sum", ctypes.c_double),
                 ("n_partitions", ctypes.c_uint32), ("n_contributions", ctypes.c_uint32),
-                ("reserved", ctypes.c_uint32 * 2)]
+                ("leader", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+
+class HistOut(ctypes.Structure):
+    """dpg_hist_out: device outputs of dpg_dataset_histograms."""
+    _fields_ = [("int_bins", ctypes.c_void_p), ("sum_count", ctypes.c_void_p),
+                ("sum_sum", ctypes.c_void_p), ("sum_max", ctypes.c_void_p),
+                ("lowers", ctypes.c_void_p)]
 
 
 class UaConfig(ctypes.Structure):
@@ -154,6 +164,9 @@ def load():
         lib.dpg_utility_analysis.argtypes = [vp, vp, vp, i64, ctypes.POINTER(UaParams), vp, vp,
                                              vp, vp, ctypes.POINTER(ctypes.c_int64), vp]
         lib.dpg_utility_analysis.restype = ctypes.c_int
+        lib.dpg_dataset_histograms.argtypes = [vp, vp, i64, vp, i64, i32,
+                                               ctypes.POINTER(HistOut), vp]
+        lib.dpg_dataset_histograms.restype = ctypes.c_int
         lib.dpg_last_stage_times.argtypes = [vp, ctypes.c_char_p, ctypes.c_size_t,
                                              ctypes.POINTER(ctypes.c_double), i32,
                                              ctypes.POINTER(ctypes.c_int32)]
@@ -244,6 +257,13 @@ class Context:
                                            report_ptr, ctypes.byref(n_out), stream)
         self.check(st, "dpg_utility_analysis")
         return n_out.value
+
+    def dataset_histograms(self, pairs_ptr, n_pairs, starts_ptr, n_partitions,
+                           pre_aggregated: bool, out: HistOut, stream):
+        st = self.lib.dpg_dataset_histograms(self.handle, pairs_ptr, n_pairs, starts_ptr,
+                                             n_partitions, int(bool(pre_aggregated)),
+                                             ctypes.byref(out), stream)
+        self.check(st, "dpg_dataset_histograms")
 
     def stage_times(self):
         names = ctypes.create_string_buffer(1024)

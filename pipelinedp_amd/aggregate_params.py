@@ -265,6 +265,37 @@ class SelectPartitionsParams:
 
 
 @dataclasses.dataclass
+class CalculatePrivateContributionBoundsParams:
+    """Parameters of DPEngine.calculate_private_contribution_bounds
+    (aggregate_params.py:113-150): the noise and budget of the COUNT /
+    PRIVACY_ID_COUNT aggregation the bound is for, the budget of the
+    calculation itself and the largest bound worth considering."""
+    aggregation_noise_kind: NoiseKind
+    aggregation_eps: float
+    aggregation_delta: float
+    calculation_eps: float
+    max_partitions_contributed_upper_bound: int
+
+    def __post_init__(self):
+        owner = "CalculatePrivateContributionBoundsParams"
+        validate_epsilon_delta(self.aggregation_eps, self.aggregation_delta, owner)
+        if self.aggregation_noise_kind is None:
+            raise ValueError("aggregation_noise_kind must be set.")
+        if self.aggregation_noise_kind == NoiseKind.GAUSSIAN and self.aggregation_delta == 0:
+            raise ValueError("The Gaussian noise requires that the aggregation_delta is "
+                             "greater than 0.")
+        validate_epsilon_delta(self.calculation_eps, 0, owner)
+        _require_positive_int(self.max_partitions_contributed_upper_bound,
+                              "max_partitions_contributed_upper_bound")
+
+
+@dataclasses.dataclass
+class PrivateContributionBounds:
+    """Contribution bounds chosen with DP (aggregate_params.py:153-163)."""
+    max_partitions_contributed: int
+
+
+@dataclasses.dataclass
 class SumParams:
     max_partitions_contributed: int
     max_contributions_per_partition: int

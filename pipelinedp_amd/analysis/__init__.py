@@ -7,3 +7,4 @@ from pipelinedp_amd.analysis.data_structures import UtilityAnalysisOptions
 from pipelinedp_amd.analysis import metrics
 from pipelinedp_amd.analysis.utility_analysis import perform_utility_analysis
 from pipelinedp_amd.analysis.utility_analysis import UtilityAnalysis
+from pipelinedp_amd.analysis import parameter_tuning

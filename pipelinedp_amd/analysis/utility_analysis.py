@@ -37,6 +37,7 @@ from pipelinedp_amd import data_extractors as dex
 from pipelinedp_amd import dp_computations as dpc
 from pipelinedp_amd import partition_selection
 from pipelinedp_amd import pipeline_backend
+from pipelinedp_amd import pre_aggregation
 from pipelinedp_amd.analysis import data_structures
 from pipelinedp_amd.analysis import metrics
 
@@ -89,8 +90,6 @@ def _check_options(options: data_structures.UtilityAnalysisOptions, extractors):
     if params.contribution_bounds_already_enforced:
         raise NotImplementedError("utility analysis when contribution bounds are already "
                                   "enforced is not supported")
-    if options.n_configurations > 64:
-        raise NotImplementedError("at most 64 configurations per sweep (one per wave lane)")
 
 
 def _noise_std(noise_kind, eps: float, delta: float, l0: float, linf: float) -> float:
@@ -170,67 +169,14 @@ class UtilityAnalysis:
     def _pairs(self, dev):
         """Sorted pre-aggregate (pairs, partition_start, P, key_table,
         public bitmap)."""
-        ctx = self.backend.ctx
-        stream = torch.cuda.current_stream(dev)
-        sptr = ctypes.c_void_p(stream.cuda_stream)
         if self.options.pre_aggregated_data:
-            return self._pairs_preaggregated(dev)
-        enc = columnar.encode(self.col, self.extractors, dev,
-                              need_values=self.extractors.value_extractor is not None,
-                              public_partitions=self.public)
-        P = enc.n_partitions
-        bound = _native.BoundParams()
-        bound.n_partitions = P
-        bound.pid_min, bound.pid_count = enc.pid_min, enc.pid_count
-        bound.rec_id_offset = enc.rec_id_offset
-        if enc.public_mask is not None:
-            bound.public_mask = enc.public_mask.data_ptr()
-        cap = max(enc.n, 1)
-        pairs = torch.empty((cap, 4), dtype=torch.float64, device=dev)  # 32 B per pair
-        starts = torch.empty(P + 1, dtype=torch.int64, device=dev)
-        with torch.cuda.device(dev):
-            n_pairs = ctx.preaggregate(
-                ctypes.c_void_p(enc.pid.data_ptr()), ctypes.c_void_p(enc.pk.data_ptr()),
-                ctypes.c_void_p(enc.value.data_ptr()) if enc.value is not None else None,
-                enc.n, bound, ctypes.c_void_p(pairs.data_ptr()), cap,
-                ctypes.c_void_p(starts.data_ptr()), sptr)
-        self.n_pairs = n_pairs
-        return pairs, starts, P, enc.key_table, enc.public_mask
-
-    def _pairs_preaggregated(self, dev):
-        """PreAggregateExtractors input: (partition key, (count, sum,
-        n_partitions)) per pair; sorted by key on ingest."""
-        rows = self.col if isinstance(self.col, list) else list(self.col)
-        ex = self.extractors
-        keys = [ex.partition_extractor(r) for r in rows]
-        pre = [ex.preaggregate_extractor(r) for r in rows]
-        ids, table, pub_ids = columnar._encode_keys(keys, torch.device("cpu"),
-                                                    None if self.public is None
-                                                    else list(self.public))
-        ids = ids.numpy()
-        P = max(len(table), 1)
-        pub_mask = None
-        if self.public is not None:
-            pub = np.zeros(P, bool)
-            pub[np.asarray(pub_ids, np.int64)] = True
-            keep = pub[ids]
-            ids, pre = ids[keep], [x for x, k in zip(pre, keep) if k]
-            bits = np.packbits(pub, bitorder="little")
-            pub_mask = torch.from_numpy(bits).to(dev)
-        order = np.argsort(ids, kind="stable")
-        n = len(order)
-        arr = np.zeros(max(n, 1), dtype=[("pk", "<u4"), ("count", "<u4"), ("sum", "<f8"),
-                                          ("np", "<u4"), ("nc", "<u4"), ("r", "<u8")])
-        if n:
-            pre_a = np.asarray(pre, dtype=np.float64).reshape(n, -1)[order]
-            arr["pk"][:n] = ids[order]
-            arr["count"][:n] = pre_a[:, 0]
-            arr["sum"][:n] = pre_a[:, 1]
-            arr["np"][:n] = pre_a[:, 2]
-        starts = np.searchsorted(ids[order], np.arange(P + 1)).astype(np.int64)
-        pairs = torch.from_numpy(arr.view(np.float64).reshape(-1, 4).copy()).to(dev)
-        self.n_pairs = n
-        return pairs, torch.from_numpy(starts).to(dev), P, table, pub_mask
+            ps = pre_aggregation.host_preaggregated_pairs(self.col, self.extractors, self.public,
+                                                          dev)
+        else:
+            ps = pre_aggregation.device_pairs(self.col, self.extractors, self.backend,
+                                              self.public, dev)
+        self.n_pairs = ps.n_pairs
+        return ps.pairs, ps.starts, ps.n_partitions, ps.key_table, ps.public_mask
 
     def _sample_mask(self, P, key_table, dev):
         prob = self.options.partitions_sampling_prob
@@ -270,13 +216,6 @@ class UtilityAnalysis:
                     t = np.ascontiguousarray(s.table, dtype=np.float64)
                     tables.append(t)
                     x.keep_table, x.table_len = t.ctypes.data, len(t)
-        up = _native.UaParams()
-        up.n_configs = C
-        up.metric_mask = sum(bit for m, bit in _BLOCKS if m in self.metrics)
-        up.public_partitions = int(self.public is not None)
-        up.configs = ctypes.addressof(cfgs)
-        up.sample_mask = sample.data_ptr() if sample is not None else None
-        up.public_mask = pub_mask.data_ptr() if pub_mask is not None else None
         slot = {agg.Metrics.SUM: 0, agg.Metrics.COUNT: 1, agg.Metrics.PRIVACY_ID_COUNT: 2}
         for i, cf in enumerate(self.configs):
             for m in self.metrics:
@@ -287,13 +226,33 @@ class UtilityAnalysis:
         keep = torch.empty((P, C), **f64) if self.public is None else None
         F = 4 + 24 * M
         rep = torch.empty((len(BUCKET_BOUNDS), F, C), **f64)
-        with torch.cuda.device(dev):
-            sptr = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-            self.n_out = ctx.utility_analysis(
-                ctypes.c_void_p(pairs.data_ptr()), ctypes.c_void_p(starts.data_ptr()), P, up,
-                ctypes.c_void_p(raw.data_ptr()), ctypes.c_void_p(err.data_ptr()),
-                ctypes.c_void_p(keep.data_ptr()) if keep is not None else None,
-                ctypes.c_void_p(rep.data_ptr()), sptr)
+        # one device pass per 64 configurations (lane = configuration); the
+        # pre-aggregate is shared, the outputs are stitched along C
+        for c0 in range(0, C, 64):
+            c1 = min(C, c0 + 64)
+            whole = c0 == 0 and c1 == C
+            up = _native.UaParams()
+            up.n_configs = c1 - c0
+            up.metric_mask = sum(bit for m, bit in _BLOCKS if m in self.metrics)
+            up.public_partitions = int(self.public is not None)
+            up.configs = ctypes.addressof(cfgs) + c0 * ctypes.sizeof(_native.UaConfig)
+            up.sample_mask = sample.data_ptr() if sample is not None else None
+            up.public_mask = pub_mask.data_ptr() if pub_mask is not None else None
+            e_c = err if whole else torch.empty((P, max(M, 1), 5, c1 - c0), **f64)
+            k_c = keep if whole or keep is None else torch.empty((P, c1 - c0), **f64)
+            r_c = rep if whole else torch.empty((len(BUCKET_BOUNDS), F, c1 - c0), **f64)
+            with torch.cuda.device(dev):
+                sptr = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+                self.n_out = ctx.utility_analysis(
+                    ctypes.c_void_p(pairs.data_ptr()), ctypes.c_void_p(starts.data_ptr()), P, up,
+                    ctypes.c_void_p(raw.data_ptr()), ctypes.c_void_p(e_c.data_ptr()),
+                    ctypes.c_void_p(k_c.data_ptr()) if k_c is not None else None,
+                    ctypes.c_void_p(r_c.data_ptr()), sptr)
+            if not whole:
+                err[..., c0:c1] = e_c
+                rep[..., c0:c1] = r_c
+                if keep is not None:
+                    keep[:, c0:c1] = k_c
         self.pairs, self.starts, self.key_table = pairs, starts, key_table
         self.sample, self.pub_mask = sample, pub_mask
         self.raw_all, self.err_all, self.keep_all, self.rep = raw, err, keep, rep

@@ -26,6 +26,7 @@
 #include "dpg_bound.h"
 #include "dpg_chunk.h"
 #include "dpg_common.h"
+#include "dpg_hist.h"
 #include "dpg_partition.h"
 #include "dpg_select.h"
 #include "dpg_utility.h"
@@ -1103,6 +1104,99 @@ int dpg_utility_analysis(dpg_ctx *ctx, const dpg_pair_entry *pairs,
         if (n_out) *n_out = run;
     }
     stage(ctx, s, "ua.end");
+    return DPG_OK;
+}
+
+int dpg_dataset_histograms(dpg_ctx *ctx, const dpg_pair_entry *pairs, int64_t n_pairs,
+                           const int64_t *partition_start, int64_t P, int32_t pre_aggregated,
+                           const dpg_hist_out *out, void *stream) {
+    static_assert(DPG_HIST_INT_BINS == kHiBins && DPG_HIST_SUM_BINS == kHsBins, "hist bins");
+    if (!ctx) return DPG_ERR_INVALID_ARG;
+    if (!out || !out->int_bins || !out->sum_count || !out->sum_sum || !out->sum_max ||
+        !out->lowers || !partition_start || P <= 0 || n_pairs < 0 || (n_pairs > 0 && !pairs))
+        return fail(ctx, DPG_ERR_INVALID_ARG, "null argument");
+    if (P >= 0xFFFFFFFFll) return fail(ctx, DPG_ERR_INVALID_ARG, "n_partitions must be < 2^32-1");
+    (void)hipSetDevice(ctx->device);
+    hipStream_t s = (hipStream_t)stream;
+    ctx->stage_names.clear();
+    ctx->n_events_used = 0;
+    ctx->last_stream = s;
+    int st = DPG_OK;
+    stage(ctx, s, "hist.begin");
+    const ItemPA *pa = reinterpret_cast<const ItemPA *>(pairs);
+    HistArgs a{};
+    a.ib = reinterpret_cast<unsigned long long *>(out->int_bins);
+    a.scount = reinterpret_cast<unsigned long long *>(out->sum_count);
+    a.ssum = out->sum_sum;
+    a.smax = reinterpret_cast<unsigned long long *>(out->sum_max);
+    a.lowers = out->lowers;
+    WS(pcount, unsigned int, "hist.pcount", P);
+    WS(minmax, unsigned long long, "hist.minmax", 2);
+    a.pcount = pcount;
+    a.minmax = minmax;
+    HIP_TRY(hipMemsetAsync(a.ib, 0, sizeof(unsigned long long) * kHiTypes * kHiBins * 3, s));
+    HIP_TRY(hipMemsetAsync(a.scount, 0, 8 * kHsBins, s));
+    HIP_TRY(hipMemsetAsync(a.ssum, 0, 8 * kHsBins, s));
+    HIP_TRY(hipMemsetAsync(a.smax, 0, 8 * kHsBins, s));
+    HIP_TRY(hipMemsetAsync(a.lowers, 0, 8 * (kHsBins + 1), s));
+    HIP_TRY(hipMemsetAsync(pcount, 0, 4 * (size_t)P, s));
+    const unsigned long long mm0[2] = {~0ull, 0ull};
+    HIP_TRY(hipMemcpyAsync(minmax, mm0, sizeof(mm0), hipMemcpyHostToDevice, s));
+    if (n_pairs == 0) {
+        stage(ctx, s, "hist.end");
+        return DPG_OK;
+    }
+    const unsigned gp = (unsigned)std::min<int64_t>((n_pairs + kHistThreads - 1) / kHistThreads,
+                                                    (int64_t)ctx->n_cu * 8);
+    if (pre_aggregated) {
+        // weights per exact n_partitions / n_contributions value: dense
+        // tables sized by the largest value present
+        uint32_t mx[2] = {0u, 0u};
+        WS(dmx, uint32_t, "hist.wmax", 2);
+        HIP_TRY(hipMemsetAsync(dmx, 0, 8, s));
+        k_pa_max<<<gp, kHistThreads, 0, s>>>(pa, n_pairs, dmx);
+        LAUNCH_CHECK();
+        HIP_TRY(hipMemcpyAsync(mx, dmx, 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (mx[0] >= (1u << 30) || mx[1] >= (1u << 30))
+            return fail(ctx, DPG_ERR_UNSUPPORTED, "n_partitions / n_contributions >= 2^30");
+        a.wlen0 = (int64_t)mx[0] + 1;
+        a.wlen1 = (int64_t)mx[1] + 1;
+        WS(w0, double, "hist.w0", a.wlen0);
+        WS(w1, double, "hist.w1", a.wlen1);
+        HIP_TRY(hipMemsetAsync(w0, 0, 8 * a.wlen0, s));
+        HIP_TRY(hipMemsetAsync(w1, 0, 8 * a.wlen1, s));
+        a.w0 = w0;
+        a.w1 = w1;
+    }
+    stage(ctx, s, "hist.pairs");
+    if (pre_aggregated) k_hist_pairs<true><<<gp, kHistThreads, 0, s>>>(pa, n_pairs, a);
+    else k_hist_pairs<false><<<gp, kHistThreads, 0, s>>>(pa, n_pairs, a);
+    LAUNCH_CHECK();
+    if (pre_aggregated) {
+        const int64_t wl = std::max(a.wlen0, a.wlen1);
+        k_hist_weights<<<(unsigned)std::min<int64_t>((wl + kHistThreads - 1) / kHistThreads,
+                                                     (int64_t)ctx->n_cu * 4),
+                         kHistThreads, 0, s>>>(a);
+        LAUNCH_CHECK();
+    }
+    stage(ctx, s, "hist.partitions");
+    k_hist_parts<<<(unsigned)std::min<int64_t>((P + kHistThreads - 1) / kHistThreads,
+                                               (int64_t)ctx->n_cu * 8),
+                   kHistThreads, 0, s>>>(partition_start, P, a);
+    LAUNCH_CHECK();
+    stage(ctx, s, "hist.sums");
+    k_hist_lowers<<<(kHsBins + kHistThreads) / kHistThreads, kHistThreads, 0, s>>>(a);
+    LAUNCH_CHECK();
+    const size_t lds = (size_t)kHsBins * (4 + 8);
+    (void)hipFuncSetAttribute((const void *)k_hist_sums, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    k_hist_sums<<<(unsigned)std::min<int64_t>((n_pairs + 1023) / 1024, (int64_t)ctx->n_cu), 1024,
+                  lds, s>>>(pa, n_pairs, a);
+    LAUNCH_CHECK();
+    k_hist_finish<<<(kHsBins + kHistThreads - 1) / kHistThreads, kHistThreads, 0, s>>>(a);
+    LAUNCH_CHECK();
+    stage(ctx, s, "hist.end");
     return DPG_OK;
 }
 

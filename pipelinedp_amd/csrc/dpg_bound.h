@@ -496,6 +496,17 @@ __global__ __launch_bounds__(kBigThreads) void k_bound_big(
     }
     mark(bp, 6, clk);
     // ---- G: emit kept pairs
+    if constexpr (kPA) {
+        // pid leader (pad0 = 1): the pair with the smallest slot of its
+        // privacy id (pidslot is dead here: no pid is over a limit)
+        for (uint32_t q = tid; q < Cq; q += kBigThreads) pidslot[q] = kNil;
+        big_sync();
+        for (uint32_t p = tid; p < Cp; p += kBigThreads) {
+            const uint64_t pkey = pairtab[p];
+            if (pkey != kEmpty64 && paircnt[p] > 0) atomicMin(&pidslot[(uint32_t)(pkey >> pkb)], p);
+        }
+        big_sync();
+    }
     Item *out = items + *item_off;
     for (uint32_t p = tid; p < Cp; p += kBigThreads) {
         const uint64_t pkey = pairtab[p];
@@ -524,7 +535,8 @@ __global__ __launch_bounds__(kBigThreads) void k_bound_big(
             const uint32_t q = (uint32_t)(pkey >> pkb);
             it.npart = pidm[q];
             it.ncontrib = pidc[q];
-            it.pad0 = it.pad1 = 0;
+            it.pad0 = pidslot[q] == p ? 1u : 0u;
+            it.pad1 = 0;
         }
         out[atomicAdd(item_cursor, 1u)] = it;
     }

@@ -497,6 +497,21 @@ __device__ __forceinline__ void bound_chunk(const R (&r)[kRPT], uint32_t n, uint
     }
     // ---- G: emit kept pairs (pair-major, dense); clear the tables for the
     // next chunk
+    if constexpr (ItemTraits<Item>::preagg) {
+        // pid leader (pad0 = 1): the pair with the smallest slot of its
+        // privacy id (pidv is dead here; phase B rewrites it per chunk)
+#pragma unroll
+        for (int j = 0; j < kQPT; ++j) {
+            const uint32_t li = tid + j * kBT;
+            if (li < npid) pidv[qlist[li]] = 0xFFFFFFFFu;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kPPT; ++j)
+            if (emit[j])
+                atomicMin(&pidv[(uint32_t)(pairtab[pslot_of[j]] >> pkb) & (kCq - 1)], pslot_of[j]);
+        __syncthreads();
+    }
     uint32_t islot[kPPT];
     wave_alloc_batch<kPPT>(&sh->nitems, emit, islot);
 #pragma unroll
@@ -518,10 +533,12 @@ __device__ __forceinline__ void bound_chunk(const R (&r)[kRPT], uint32_t n, uint
             it.nsq = need_v ? acc_nsq[p] : 0.0;
         }
         if constexpr (ItemTraits<Item>::preagg) {
-            const uint32_t pm = pidm[(uint32_t)(pairtab[p] >> pkb) & (kCq - 1)];
+            const uint32_t q = (uint32_t)(pairtab[p] >> pkb) & (kCq - 1);
+            const uint32_t pm = pidm[q];
             it.npart = pm & 0xFFFFu;
             it.ncontrib = pm >> 16;
-            it.pad0 = it.pad1 = 0;
+            it.pad0 = pidv[q] == p ? 1u : 0u;
+            it.pad1 = 0;
         }
         items[slot] = it;
     }

@@ -864,6 +864,20 @@ bool overp[kWQPL];
     }
     // ---- G: emit kept pairs; clear the key table
     {
+        if constexpr (ItemTraits<Item>::preagg) {
+            // pid leader: the pair with the smallest dense id of its privacy
+            // id carries pad0 = 1, so dataset histograms count every privacy
+            // id once (pidv, the pid hashes, is dead here and is rewritten
+            // for the next chunk's occupied slots)
+#pragma unroll
+            for (int j = 0; j < kWQPL; ++j) pidv[qv[j]] = 0xFFFFFFFFu;
+            wave_sync();
+#pragma unroll
+            for (int j = 0; j < kWPPL && j < (int)jn; ++j)
+                if ((keptm >> j) & 1u)
+                    atomicMin(&pidv[(uint32_t)(pkv[j] >> pkb) & (kWCq - 1)], lane + 64u * j);
+            wave_sync();
+        }
         double a0[kWPPL], a1[kWPPL], a2[kWPPL];
 #pragma unroll
         for (int j = 0; j < kWPPL && j < (int)jn; ++j) {
@@ -888,10 +902,12 @@ bool overp[kWQPL];
                     it.nsq = a2[j];
                 }
                 if constexpr (ItemTraits<Item>::preagg) {
-                    const uint32_t pm = pidm[(uint32_t)(pkv[j] >> pkb) & (kWCq - 1)];
+                    const uint32_t q = (uint32_t)(pkv[j] >> pkb) & (kWCq - 1);
+                    const uint32_t pm = pidm[q];
                     it.npart = pm & 0xFFFFu;
                     it.ncontrib = pm >> 16;
-                    it.pad0 = it.pad1 = 0;
+                    it.pad0 = pidv[q] == lane + 64u * j ? 1u : 0u;
+                    it.pad1 = 0;
                 }
                 items[nitems + lanes_below(be)] = it;
             }

@@ -8,9 +8,12 @@ diversity b = l1/eps (:431-478), the mean / variance parameter plumbing
 explain report.  Per-partition noise itself is drawn on the GPU
 (csrc/dpg_select.h), never here.
 """
+import abc
 import dataclasses
 import math
-from typing import Any, List, Optional, Tuple
+from typing import Any, List, Optional, Sequence, Tuple
+
+import numpy as np
 
 from pipelinedp_amd import aggregate_params as agg
 
@@ -190,3 +193,59 @@ def noise_scale(noise_kind: agg.NoiseKind, eps: float, delta: float, l0: float,
     if noise_kind == agg.NoiseKind.LAPLACE:
         return compute_l1_sensitivity(l0, linf) / eps
     return compute_sigma(eps, delta, compute_l2_sensitivity(l0, linf))
+
+
+def compute_count_noise_std(noise_kind: agg.NoiseKind, eps: float, delta: float, l0: float,
+                            linf: float) -> float:
+    """Noise standard deviation of a COUNT with sensitivities (l0, linf)
+    (dp_computations.py:369-388: Laplace b * sqrt(2), Gaussian sigma)."""
+    if noise_kind == agg.NoiseKind.LAPLACE:
+        return compute_l1_sensitivity(l0, linf) / eps * math.sqrt(2)
+    return compute_sigma(eps, delta, compute_l2_sensitivity(l0, linf))
+
+
+class ExponentialMechanism:
+    """Chooses one of a list of candidates with probability proportional to
+    exp(eps * score / (sensitivity, doubled unless the score is monotonic))
+    (dp_computations.py:662-716).  The scores are host work over at most a
+    few thousand candidates."""
+
+    class ScoringFunction(abc.ABC):
+
+        @abc.abstractmethod
+        def score(self, k) -> float:
+            """Higher is more likely."""
+
+        @property
+        @abc.abstractmethod
+        def global_sensitivity(self) -> float:
+            """Global sensitivity of the score."""
+
+        @property
+        @abc.abstractmethod
+        def is_monotonic(self) -> bool:
+            """Whether score(D, k) moves the same way for every k between
+            neighbouring datasets."""
+
+        def scores(self, candidates: Sequence) -> np.ndarray:
+            """All scores at once (override for a vectorised form)."""
+            return np.array([self.score(k) for k in candidates], dtype=np.float64)
+
+    def __init__(self, scoring_function: "ExponentialMechanism.ScoringFunction"):
+        self._scoring_function = scoring_function
+
+    def apply(self, eps: float, inputs_to_score_col: List[Any]) -> Any:
+        probs = self._calculate_probabilities(eps, inputs_to_score_col)
+        return np.random.default_rng().choice(inputs_to_score_col, p=probs)
+
+    def _calculate_probabilities(self, eps: float, inputs_to_score_col: List[Any]) -> np.ndarray:
+        scores = self._scoring_function.scores(inputs_to_score_col)
+        denominator = self._scoring_function.global_sensitivity
+        if not self._scoring_function.is_monotonic:
+            denominator *= 2
+        # shifted by the best score: the same distribution as the reference's
+        # exp(score * eps / d) / sum, without the 0 / 0 it hits when every
+        # weight underflows (very negative scores)
+        z = scores * eps / denominator
+        weights = np.exp(z - z.max())
+        return weights / weights.sum()

@@ -18,7 +18,10 @@ from pipelinedp_amd import combiners
 from pipelinedp_amd import data_extractors as dex
 from pipelinedp_amd import device_aggregate
 from pipelinedp_amd import pipeline_backend
+from pipelinedp_amd import pre_aggregation
+from pipelinedp_amd import private_contribution_bounds
 from pipelinedp_amd import report_generator
+from pipelinedp_amd.dataset_histograms import computing_histograms
 
 
 def _as_collection(public_partitions):
@@ -168,10 +171,37 @@ class DPEngine:
                 params.budget_weight)
             return self._annotate(result, params=params, budget=budget)
 
-    def calculate_private_contribution_bounds(self, *args, **kwargs):
-        raise NotImplementedError(
-            "calculate_private_contribution_bounds is not part of the MI355X hot "
-            "path (SURVEY.md 8(f), rank 4)")
+    # --------------------------------------- private contribution bounds
+    def calculate_private_contribution_bounds(
+            self, col, params: agg.CalculatePrivateContributionBoundsParams,
+            data_extractors: dex.DataExtractors, partitions, partitions_already_filtered=False):
+        """DP max_partitions_contributed for COUNT / PRIVACY_ID_COUNT
+        (dp_engine.py:432-484): the L0 histogram of the rows restricted to
+        `partitions` (device: pre-aggregate + histogram kernels), then the
+        exponential mechanism over the candidate bounds.  Returns a
+        1-element collection of PrivateContributionBounds."""
+        _check_col(col)
+        if params is None:
+            raise ValueError("params must be set to a valid "
+                             "CalculatePrivateContributionBoundsParams")
+        if not isinstance(params, agg.CalculatePrivateContributionBoundsParams):
+            raise TypeError("params must be set to a valid "
+                            "CalculatePrivateContributionBoundsParams")
+        _check_data_extractors(data_extractors)
+        self._require_device_backend()
+        partitions = _as_collection(partitions)
+        backend = self._backend
+
+        def histograms():
+            ps = pre_aggregation.device_pairs(
+                col, data_extractors, backend,
+                None if partitions_already_filtered else partitions, backend.device)
+            return computing_histograms.histograms_from_pairs(ps, backend, pre_aggregated=False)
+
+        calc = private_contribution_bounds.PrivateL0Calculator(
+            params, partitions, computing_histograms._OneElement(histograms), backend)
+        return computing_histograms._OneElement(lambda: agg.PrivateContributionBounds(
+            max_partitions_contributed=calc.calculate()[0]))
 
     # ------------------------------------------------------------- checks
     def _check_aggregate_params(self, col, params, data_extractors):
