@@ -169,11 +169,47 @@ struct SrcItems {
 };
 
 // ------------------------------------------------------------ tile table
-// One thread per segment: allocate ceil(n / tile) tiles.
+// One thread per segment: allocate ceil(n / tile) tiles.  With XCD queues
+// (xq != null) the segment's tile ids are also appended to the queue of XCD
+// s % 8, so that one XCD's workgroups take all tiles of a segment together
+// (k_scatter's XCD-local mode).
+struct XcdQueues {
+    uint32_t *q;      // [8][stride] global tile ids
+    uint32_t *n;      // [8] queue lengths
+    uint32_t *next;   // [8] work counters (zeroed)
+    uint32_t stride;
+};
+
+// One segment cut into many one-sub-tile tiles (level 1 in XCD-local mode):
+// one thread per tile.  Groups of G consecutive tiles go to the XCD queues
+// round-robin, so the ~G workgroups of one XCD write adjacent runs of every
+// digit at the same time (they meet in that XCD's L2).
+__global__ void k_build_tiles_single(int64_t n, int64_t tile, uint32_t G, TileDesc *tiles,
+                                     uint32_t *seg_tile_base, uint32_t *seg_ntiles,
+                                     uint32_t *ntiles_total, XcdQueues xq) {
+    const uint32_t nt = (uint32_t)((n + tile - 1) / tile);
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t == 0) {
+        seg_tile_base[0] = 0;
+        seg_ntiles[0] = nt;
+        *ntiles_total = nt;
+    }
+    if (t >= nt) return;
+    TileDesc d;
+    d.begin = (int64_t)t * tile;
+    d.end = min((int64_t)(t + 1) * tile, n);
+    d.seg = 0;
+    d.pad = 0;
+    tiles[t] = d;
+    const uint32_t g = t / G, x = g & 7u;
+    xq.q[(size_t)x * xq.stride + (g >> 3) * G + t % G] = t;
+    atomicAdd(&xq.n[x], 1u);
+}
+
 __global__ void k_build_tiles(const int64_t *seg_start, const uint32_t *seg_cnt,
                               const int64_t *seg_cnt64, uint32_t S, int64_t tile,
                               TileDesc *tiles, uint32_t *seg_tile_base, uint32_t *seg_ntiles,
-                              uint32_t *ntiles_total) {
+                              uint32_t *ntiles_total, XcdQueues xq = XcdQueues{}) {
     uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= S) return;
     int64_t st = seg_start ? seg_start[s] : 0;
@@ -189,6 +225,11 @@ __global__ void k_build_tiles(const int64_t *seg_start, const uint32_t *seg_cnt,
         d.seg = s;
         d.pad = 0;
         tiles[b + j] = d;
+    }
+    if (xq.q && nt) {
+        const uint32_t x = s & 7u;
+        const uint32_t qb = atomicAdd(&xq.n[x], nt);
+        for (uint32_t j = 0; j < nt; ++j) xq.q[(size_t)x * xq.stride + qb + j] = b + j;
     }
 }
 
@@ -228,16 +269,21 @@ __global__ __launch_bounds__(kPartThreads) void k_hist(Src src_in, const TileDes
 }
 
 // ---------------------------------------------------------------- scan
-// grid (S, ceil(F/64)); 16 waves split a segment's tiles, lane = digit.
-// hist[t][d] <- exclusive prefix over the segment's tiles; tot[s][d] = total.
+// grid (S, ceil(F/64), C); 16 waves split chunk c of a segment's tiles (C
+// chunks of ceil(nt / C) tiles), lane = digit.  hist[t][d] <- exclusive
+// prefix over the chunk's tiles; ctot[s][c][d] = the chunk's total (C = 1:
+// the segment total).
 __global__ __launch_bounds__(1024) void k_scan_tiles(const uint32_t *seg_tile_base,
                                                      const uint32_t *seg_ntiles, uint32_t F,
-                                                     uint32_t *hist, uint32_t *tot) {
+                                                     uint32_t *hist, uint32_t *ctot) {
     __shared__ uint32_t part[16][64];
-    const uint32_t s = blockIdx.x;
+    const uint32_t s = blockIdx.x, c = blockIdx.z, C = gridDim.z;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint32_t d = blockIdx.y * 64 + lane;
-    const uint32_t nt = seg_ntiles[s], tb = seg_tile_base[s];
+    const uint32_t nt_all = seg_ntiles[s];
+    const uint32_t per = (nt_all + C - 1) / C;
+    const uint32_t c0 = min(nt_all, c * per), c1 = min(nt_all, c0 + per);
+    const uint32_t nt = c1 - c0, tb = seg_tile_base[s] + c0;
     const uint32_t ch = (nt + 15) / 16;
     const uint32_t t0 = min(nt, w * ch), t1 = min(nt, (w + 1) * ch);
     uint32_t acc = 0;
@@ -259,8 +305,24 @@ __global__ __launch_bounds__(1024) void k_scan_tiles(const uint32_t *seg_tile_ba
             hist[o] = run;
             run += x;
         }
-        if (w == 0) tot[(size_t)s * F + d] = total;
+        if (w == 0) ctot[((size_t)s * C + c) * F + d] = total;
     }
+}
+
+// C > 1 chunks: ctot[s][c][d] <- exclusive prefix over c (the chunk base the
+// scatter adds to its tile offsets), tot[s][d] = the segment total.
+__global__ void k_scan_chunks(uint32_t S, uint32_t C, uint32_t F, uint32_t *ctot, uint32_t *tot) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= S * F) return;
+    const uint32_t s = i / F, d = i % F;
+    uint32_t run = 0;
+    for (uint32_t c = 0; c < C; ++c) {
+        uint32_t &x = ctot[((size_t)s * C + c) * F + d];
+        const uint32_t v = x;
+        x = run;
+        run += v;
+    }
+    tot[(size_t)s * F + d] = run;
 }
 
 // Block-wide exclusive scan of one value per thread (1024 threads).
@@ -446,12 +508,13 @@ __device__ __forceinline__ T from_words(const Words<T> &x) {
     return r;
 }
 
-// LDS bytes of one k_scatter instantiation.
+// LDS bytes of one k_scatter instantiation (one dummy staging slot past the
+// sub-tile for records that are dropped).
 template <class Src, class Rec, int IPT, int FMAX>
 constexpr size_t scatter_lds() {
-    return (size_t)sizeof(Rec) * kScatThreads * IPT +
-           (Src::kDigitFromRec ? 0 : a16((size_t)2 * kScatThreads * IPT)) + (size_t)FMAX * 12 +
-           80;
+    return (size_t)sizeof(Rec) * (kScatThreads * IPT + 1) +
+           (Src::kDigitFromRec ? 0 : a16((size_t)2 * (kScatThreads * IPT + 1))) +
+           (size_t)FMAX * 12 + 80;
 }
 
 // kAgg: wave-aggregated ranking (few digits) instead of one LDS atomic per
@@ -461,26 +524,57 @@ template <class Src, class Rec, int IPT, int FMAX, bool kAgg>
 __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const TileDesc *tiles,
                                                           const uint32_t *ntiles, uint32_t F,
                                                           uint32_t bits, const uint32_t *off,
-                                                          const int64_t *base, Rec *out) {
+                                                          const int64_t *base, Rec *out,
+                                                          XcdQueues xq = XcdQueues{},
+                                                          const uint32_t *cbase = nullptr,
+                                                          const uint32_t *seg_tile_base = nullptr,
+                                                          const uint32_t *seg_ntiles = nullptr,
+                                                          uint32_t C = 1) {
     constexpr int SUB = kScatThreads * IPT;
     constexpr bool kSD = !Src::kDigitFromRec;
     using W = Words<Rec>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    W *stage = reinterpret_cast<W *>(smem);
-    uint16_t *sdig = reinterpret_cast<uint16_t *>(smem + sizeof(Rec) * SUB);
-    const size_t o = sizeof(Rec) * SUB + (kSD ? a16((size_t)2 * SUB) : 0);
+    W *stage = reinterpret_cast<W *>(smem);  // [SUB + 1]: slot SUB takes dropped records
+    uint16_t *sdig = reinterpret_cast<uint16_t *>(smem + sizeof(Rec) * (SUB + 1));
+    const size_t o = sizeof(Rec) * (SUB + 1) + (kSD ? a16((size_t)2 * (SUB + 1)) : 0);
     uint32_t *cnt = reinterpret_cast<uint32_t *>(smem + o);
     uint32_t *dstart = cnt + FMAX;
     uint32_t *cur = dstart + FMAX + 1;  // output positions (n < 2^32 per device)
     uint32_t *sh16 = cur + FMAX;
 
-    const uint32_t t = blockIdx.x;
-    if (t >= *ntiles) return;
-    const TileDesc td = tiles[t];
+    // persistent over the tiles.  XCD-local mode (xq.q): workgroup b serves
+    // the queue of XCD b % 8 (round-robin placement), taking the next tile id
+    // by one atomic per tile, so an XCD's workgroups work on the same
+    // segments at the same time and their runs meet in that XCD's L2
+    const uint32_t nt = *ntiles;
     const int tid = threadIdx.x;
+    __shared__ uint32_t sh_next;
+    const uint32_t xq_id = blockIdx.x & 7u;
+    const uint32_t xq_len = xq.q ? xq.n[xq_id] : 0u;
+    for (uint32_t it = blockIdx.x;; it += gridDim.x) {
+    uint32_t t;
+    if (xq.q) {
+        __syncthreads();  // every thread has read the previous sh_next
+        if (tid == 0) sh_next = atomicAdd(&xq.next[xq_id], 1u);
+        __syncthreads();
+        const uint32_t w = __builtin_amdgcn_readfirstlane(sh_next);
+        if (w >= xq_len) break;
+        t = __builtin_amdgcn_readfirstlane(xq.q[(size_t)xq_id * xq.stride + w]);
+    } else {
+        if (it >= nt) break;
+        t = it;
+    }
+    const TileDesc td = tiles[t];
     Src src = src_in;  // per-thread copy (sources may cache lookup state)
+    __syncthreads();   // the previous tile's write-out has read cur / dstart
+    // chunked tile scan: the tile's offset is relative to its chunk
+    const uint32_t *cb = nullptr;
+    if (cbase) {
+        const uint32_t nta = seg_ntiles[td.seg], per = (nta + C - 1) / C;
+        cb = cbase + ((size_t)td.seg * C + (t - seg_tile_base[td.seg]) / per) * F;
+    }
     for (uint32_t d = tid; d < F; d += kScatThreads) {
-        cur[d] = (uint32_t)(base[(size_t)td.seg * F + d] + off[(size_t)t * F + d]);
+        cur[d] = (uint32_t)(base[(size_t)td.seg * F + d] + off[(size_t)t * F + d] + (cb ? cb[d] : 0u));
         cnt[d] = 0;
     }
     // software pipeline: the raw loads of sub-tile j + 1 are issued right
@@ -489,6 +583,9 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
     // Loads are unconditional with the index clamped into the sub-tile (a
     // guarded load becomes a branch with its own vmcnt(0) wait, serialising
     // the sub-tile's loads); lanes past the end re-read the last record.
+    // Every LDS step below is likewise branch-free: a predicated LDS access
+    // whose result is used becomes a branch with an lgkmcnt(0) wait inside,
+    // which serialises the IPT accesses of a thread.
     typename Src::Raw raw[IPT];
     {
         const uint32_t lim = (uint32_t)min<int64_t>(SUB, td.end - td.begin);
@@ -503,17 +600,22 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
         uint32_t dr[IPT];  // digit | rank << 12, or ~0 for a dropped record
         if constexpr (!kAgg) {
             // wide fan-out: one LDS atomic per record ranks it (order inside
-            // a digit is free); all IPT atomics are in flight together
+            // a digit is free); all IPT atomics are in flight together, a
+            // dropped record adds 0 to digit 0
+            uint32_t dg[IPT];
+            bool okv[IPT];
 #pragma unroll
             for (int j = 0; j < IPT; ++j) {
                 const uint32_t o = j * kScatThreads + tid;
                 uint32_t d = 0;
-                const bool ok = o < lim && src.decode(raw[j], sb + o, rec[j], d);
-                dr[j] = ok ? d : ~0u;
+                okv[j] = o < lim && src.decode(raw[j], sb + o, rec[j], d);
+                dg[j] = okv[j] ? d : 0u;
             }
+            uint32_t rk[IPT];
 #pragma unroll
-            for (int j = 0; j < IPT; ++j)
-                if (dr[j] != ~0u) dr[j] |= atomicAdd(&cnt[dr[j]], 1u) << 12;
+            for (int j = 0; j < IPT; ++j) rk[j] = atomicAdd(&cnt[dg[j]], okv[j] ? 1u : 0u);
+#pragma unroll
+            for (int j = 0; j < IPT; ++j) dr[j] = okv[j] ? (dg[j] | (rk[j] << 12)) : ~0u;
         } else {
             // few digits: wave-aggregated ranking avoids same-address
             // serialisation
@@ -529,14 +631,17 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
         __syncthreads();
         const uint32_t total =
             scatter_scan_update<kScatThreads, FMAX / kScatThreads>(cnt, dstart, cur, F, sh16);
+        {
+            uint32_t ds[IPT];
 #pragma unroll
-        for (int j = 0; j < IPT; ++j)
-            if (dr[j] != ~0u) {
-                const uint32_t d = dr[j] & 0xFFFu;
-                const uint32_t pos = dstart[d] + (dr[j] >> 12);
+            for (int j = 0; j < IPT; ++j) ds[j] = dstart[dr[j] != ~0u ? (dr[j] & 0xFFFu) : 0u];
+#pragma unroll
+            for (int j = 0; j < IPT; ++j) {
+                const uint32_t pos = dr[j] != ~0u ? ds[j] + (dr[j] >> 12) : (uint32_t)SUB;
                 stage[pos] = to_words(rec[j]);
-                if constexpr (kSD) sdig[pos] = (uint16_t)d;
+                if constexpr (kSD) sdig[pos] = (uint16_t)(dr[j] & 0xFFFu);
             }
+        }
         __syncthreads();
         const int64_t nb = sb + SUB;
         const uint32_t nlim = (uint32_t)max<int64_t>(0, min<int64_t>(SUB, td.end - nb));
@@ -545,31 +650,45 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
             for (int j = 0; j < IPT; ++j)
                 raw[j] = src.fetch(nb + min((uint32_t)(j * kScatThreads + tid), nlim - 1));
         }
-        // write-out in batches of WB staged records per thread: the LDS reads
-        // of a batch are in flight together, stores are predicated
+        // write-out in batches of WB staged records per thread, branch-free:
+        // slots past the end repeat the last staged record, whose store they
+        // duplicate (same value, same address)
         constexpr int WB = IPT < DPG_SCAT_WB ? IPT : DPG_SCAT_WB;
         for (uint32_t k0 = 0; k0 < total; k0 += WB * kScatThreads) {
             W x[WB];
-            uint32_t dd[WB];
+            uint32_t dd[WB], kc[WB];
 #pragma unroll
             for (int u = 0; u < WB; ++u) {
-                const uint32_t k = min(k0 + u * kScatThreads + tid, total - 1);
-                x[u] = stage[k];
-                if constexpr (kSD) dd[u] = sdig[k];
-                else dd[u] = src.digit(from_words<Rec>(x[u]));
+                kc[u] = min(k0 + u * kScatThreads + tid, total - 1);
+                x[u] = stage[kc[u]];
+                if constexpr (kSD) dd[u] = sdig[kc[u]];
             }
+            if constexpr (!kSD) {
+#pragma unroll
+                for (int u = 0; u < WB; ++u) dd[u] = src.digit(from_words<Rec>(x[u]));
+            }
+            uint32_t c1[WB], c2[WB];
 #pragma unroll
             for (int u = 0; u < WB; ++u) {
-                const uint32_t k = k0 + u * kScatThreads + tid;
-                // cur already includes this sub-tile: its run ends at cur[d]
-                const uint32_t dst = cur[dd[u]] - dstart[dd[u] + 1] + k;
-                // (non-temporal loads / stores measured slower: the partial
-                // lines of the runs merge in L2)
-                if (k < total) *reinterpret_cast<W *>(&out[dst]) = x[u];
+                c1[u] = cur[dd[u]];
+                c2[u] = dstart[dd[u] + 1];
             }
+            // cur already includes this sub-tile: its run ends at cur[d]
+            // (non-temporal loads / stores measured slower: the partial
+            // lines of the runs merge in L2)
+#ifdef DPG_SCAT_LINEAR
+            // timing experiment only (wrong output): contiguous writes
+#pragma unroll
+            for (int u = 0; u < WB; ++u)
+                *reinterpret_cast<W *>(&out[(uint32_t)(sb - td.begin) + (uint32_t)td.begin + kc[u] + 0u * (c1[u] - c2[u])]) = x[u];
+#else
+#pragma unroll
+            for (int u = 0; u < WB; ++u) *reinterpret_cast<W *>(&out[c1[u] - c2[u] + kc[u]]) = x[u];
+#endif
         }
         // the next sub-tile's first barrier (after its ranking) orders this
         // write-out's LDS reads before the next scan and staging
+    }
     }
 }
 

@@ -72,11 +72,15 @@ struct WaveLayout {
 #ifndef DPG_RT_W
 #define DPG_RT_W 8
 #endif
+// candidate bounds: round-0 mpc candidates ~ k + E0 sqrt(k) + E0 per pid,
+// pre-filter ~ CAND x (k + 2 sqrt(k) + 2) records per pid (same-box A/B,
+// config 2 / config 4 bound ms: (2.0, 2.0) 14.2 / 31.7; (1.5, 1.25) 13.1 /
+// 29.6; (1.5, 1.0) 13.0 / 29.4-29.6; (1.0, 2.0) 19.9 -- restarts)
 #ifndef DPG_E0_C
-#define DPG_E0_C 2.0f
+#define DPG_E0_C 1.25f
 #endif
 #ifndef DPG_CAND_C
-#define DPG_CAND_C 2.0f
+#define DPG_CAND_C 1.5f
 #endif
 
 // Heavy chunks (k_heavy_filter): the candidate records of one privacy id
