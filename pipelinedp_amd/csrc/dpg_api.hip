@@ -229,7 +229,11 @@ int run_level(dpg_ctx *ctx, hipStream_t s, const Src &src, uint32_t S, const int
     stage(ctx, s, (t + ":hist").c_str());
     if (single) {
         const uint32_t nt = (uint32_t)((n_upper + tile - 1) / tile);
-        k_build_tiles_single<<<(nt + 255) / 256, 256, 0, s>>>(n_upper, tile, (uint32_t)(ctx->n_cu / 8),
+#ifndef DPG_L1_GROUP
+#define DPG_L1_GROUP 1
+#endif
+        k_build_tiles_single<<<(nt + 255) / 256, 256, 0, s>>>(n_upper, tile,
+                                                             (uint32_t)(DPG_L1_GROUP * ctx->n_cu / 8),
                                                              tiles, stb, snt, ntiles_dev, xq);
     } else {
         k_build_tiles<<<(S + 255) / 256, 256, 0, s>>>(seg_start, seg_cnt, seg_cnt64, S, tile, tiles,

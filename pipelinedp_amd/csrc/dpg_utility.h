@@ -135,6 +135,10 @@ __global__ __launch_bounds__(64) void k_ua_accumulate(const ItemPA *pairs,
     for (int64_t b = lo; b < hi; b += 64) {
         const int64_t i = b + c < hi ? b + c : hi - 1;
         const ItemPA mine = pairs[i];
+        // 1 / n_partitions of the lane's pair, broadcast below: one division
+        // per pair instead of one per (pair, configuration)
+        const double inv_mine = mine.npart > 0 ? 1.0 / (double)mine.npart : 0.0;
+        const long long inv_bits = __double_as_longlong(inv_mine);
         const int m = (int)(hi - b < 64 ? hi - b : 64);
         for (int j = 0; j < m; ++j) {
             const uint32_t pk = __builtin_amdgcn_readlane(mine.pk, j);
@@ -149,13 +153,15 @@ __global__ __launch_bounds__(64) void k_ua_accumulate(const ItemPA *pairs,
             }
             if (skip) continue;
             const uint32_t cnt = __builtin_amdgcn_readlane(mine.cnt, j);
-            const uint32_t np = __builtin_amdgcn_readlane(mine.npart, j);
+            const uint32_t ilo = __builtin_amdgcn_readlane((uint32_t)inv_bits, j);
+            const uint32_t ihi = __builtin_amdgcn_readlane((uint32_t)(inv_bits >> 32), j);
+            const double inv = __longlong_as_double((long long)(((uint64_t)ihi << 32) | ilo));
             const uint32_t slo = __builtin_amdgcn_readlane((uint32_t)__double_as_longlong(mine.sum), j);
             const uint32_t shi =
                 __builtin_amdgcn_readlane((uint32_t)(__double_as_longlong(mine.sum) >> 32), j);
             const double s = __longlong_as_double((long long)(((uint64_t)shi << 32) | slo));
             // l0 keep probability of this pair (per_partition_combiners.py:203-205)
-            const double p = np > 0 ? fmin(1.0, cf.mpc / (double)np) : 0.0;
+            const double p = fmin(1.0, cf.mpc * inv);
             const double q = p * (1.0 - p);
             e += p;
             v += q;
@@ -225,17 +231,40 @@ __device__ __forceinline__ double ua_G(double x, double skew) {
 constexpr int kPgfB = 8;                                  // coefficients per block
 constexpr int kPgfNB = (kUaMaxExact + kPgfB) / kPgfB;     // 13 blocks: 104 >= 101
 
+// Range [i0, i1] of privacy-id counts whose keep probability is strictly
+// between 0 and 1 (below i0 it is 0, above i1 exactly 1.0 in double).
+__device__ __forceinline__ void ua_pi_range(const UaConfig &cf, int64_t &i0, int64_t &i1) {
+    i0 = cf.pre_threshold > 0 ? cf.pre_threshold : 1;
+    const int64_t sh = cf.pre_threshold > 0 ? cf.pre_threshold - 1 : 0;  // i -> i - pre + 1
+    if (cf.strategy == DPG_SELECT_TRUNCATED_GEOMETRIC) {
+        i1 = cf.table_len - 1 + sh;  // pi = 1.0 beyond the table
+    } else if (cf.strategy == DPG_SELECT_LAPLACE_THRESHOLD) {
+        // 0.5 exp(-x) < 2^-54 for x > 37.5
+        i1 = (int64_t)ceil(cf.threshold + 37.5 * cf.scale) + sh;
+    } else {
+        // 0.5 erfc(-z / sqrt 2) rounds to 1.0 for z > 8.5
+        i1 = (int64_t)ceil(cf.threshold + 8.5 * cf.scale) + sh;
+    }
+}
+
 __global__ __launch_bounds__(64) void k_ua_select(const ItemPA *pairs, const int64_t *pstart,
                                                   UaArgs a) {
     const int c = (int)__lane_id();
     const int64_t C64 = a.n_configs;
     const bool lane_on = c < a.n_configs;
     const UaConfig cf = a.cfg[lane_on ? c : 0];
+    int64_t i0, i1;
+    ua_pi_range(cf, i0, i1);
     for (int64_t k = blockIdx.x; k < a.P; k += gridDim.x) {
         const int64_t b = pstart[k], n = pstart[k + 1] - b;
         if (n == 0 || (a.sample_mask && !bit_of(a.sample_mask, k))) continue;
         double keep = 0.0;
         if (n <= kUaMaxExact) {
+            // 1 / n_partitions of pairs lane and lane + 64, broadcast below
+            const uint32_t n0 = pairs[b + min((int64_t)c, n - 1)].npart;
+            const uint32_t n1 = pairs[b + min((int64_t)c + 64, n - 1)].npart;
+            const long long r0 = __double_as_longlong(n0 > 0 ? 1.0 / (double)n0 : 0.0);
+            const long long r1 = __double_as_longlong(n1 > 0 ? 1.0 / (double)n1 : 0.0);
             // exact PMF: coefficients of prod_j (1 - p_j + p_j x) in registers;
             // pair j touches coefficients 0..j+1 only, so blocks above that
             // are skipped (j is wave-uniform: uniform branches)
@@ -243,8 +272,12 @@ __global__ __launch_bounds__(64) void k_ua_select(const ItemPA *pairs, const int
 #pragma unroll
             for (int i = 0; i < kPgfB * kPgfNB; ++i) co[i] = i == 0 ? 1.0 : 0.0;
             for (int64_t j = 0; j < n; ++j) {
-                const uint32_t np = pairs[b + j].npart;
-                const double p = np > 0 ? fmin(1.0, cf.mpc / (double)np) : 0.0;
+                const long long rb = j < 64 ? r0 : r1;
+                const int jl = (int)(j & 63);
+                const uint32_t lo32 = __builtin_amdgcn_readlane((uint32_t)rb, jl);
+                const uint32_t hi32 = __builtin_amdgcn_readlane((uint32_t)(rb >> 32), jl);
+                const double inv = __longlong_as_double((long long)(((uint64_t)hi32 << 32) | lo32));
+                const double p = fmin(1.0, cf.mpc * inv);
                 const double q = 1.0 - p;
                 const int top = (int)j + 1;
 #pragma unroll
@@ -267,16 +300,26 @@ __global__ __launch_bounds__(64) void k_ua_select(const ItemPA *pairs, const int
             if (sd == 0.0) {
                 keep = ua_pi(cf, a.tables, (int64_t)rint(mean));
             } else {
+                // the refined normal approximation's PMF over [st, en]
+                // (poisson_binomial.py:61-83) dotted with pi; only counts
+                // with 0 < pi < 1 are evaluated one by one: below i0 pi is 0,
+                // above i1 it is 1 and the remaining mass telescopes to
+                // G(en) - G(i1) (the same sum of CDF differences)
                 const double skew = mm[2 * C64] / (sd * sd * sd);
                 const int64_t st = (int64_t)fmax(0.0, floor(mean - 8.0 * sd));
                 const int64_t en = (int64_t)fmin((double)n, rint(mean + 8.0 * sd));
-                double prev = fmin(1.0, fmax(0.0, ua_G(((double)(st - 1) + 0.5 - mean) / sd, skew)));
-                for (int64_t i = st; i <= en; ++i) {
-                    const double cur =
-                        fmin(1.0, fmax(0.0, ua_G(((double)i + 0.5 - mean) / sd, skew)));
+                auto Gc = [&](int64_t i) {
+                    return fmin(1.0, fmax(0.0, ua_G(((double)i + 0.5 - mean) / sd, skew)));
+                };
+                const int64_t a0 = st > i0 ? st : i0;
+                const int64_t a1 = en < i1 ? en : i1;
+                double prev = a0 <= a1 ? Gc(a0 - 1) : 0.0;
+                for (int64_t i = a0; i <= a1; ++i) {
+                    const double cur = Gc(i);
                     keep += (cur - prev) * ua_pi(cf, a.tables, i);
                     prev = cur;
                 }
+                if (en > i1) keep += Gc(en) - Gc(st > i1 ? st - 1 : i1);
             }
         }
         if (lane_on) a.keep[k * C64 + c] = keep;
