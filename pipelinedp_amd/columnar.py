@@ -97,12 +97,23 @@ def _integer_like(x) -> bool:
     return np.asarray(x).dtype.kind in "iu"
 
 
+def _is_int_key(k) -> bool:
+    return isinstance(k, (int, np.integer)) and not isinstance(k, bool)
+
+
 def _encode_keys(values, device, extra=None):
     """Dictionary-encodes arbitrary keys; returns (ids tensor, key table,
     ids of `extra`)."""
     if isinstance(values, torch.Tensor) and _integer_like(values):
-        both = values if extra is None else torch.cat(
-            [values, torch.as_tensor(np.asarray(list(extra), dtype=np.int64), device=values.device)])
+        extra_i = None
+        if extra is not None:
+            extra = list(extra)
+            if not all(_is_int_key(k) for k in extra):
+                # integer data keys, public partitions with other keys: the
+                # general (object) encoding; those partitions come out empty
+                return _encode_keys(values.cpu().numpy().astype(object), device, extra)
+            extra_i = torch.as_tensor(np.asarray(extra, dtype=np.int64), device=values.device)
+        both = values if extra is None else torch.cat([values, extra_i])
         uniq, inv = torch.unique(both, return_inverse=True)
         n = values.numel()
         return (inv[:n].to(torch.int64).to(device), uniq.cpu().numpy(),
@@ -136,10 +147,19 @@ def _public_id_tensor(public_partitions, device) -> Optional[torch.Tensor]:
     return None
 
 
+def _check_public_range(lo: int, hi: int, P: int) -> None:
+    if lo < 0 or hi >= P:
+        raise ValueError(
+            f"public partition id {lo if lo < 0 else hi} is outside [0, n_partitions={P}): with "
+            f"ColumnarData(n_partitions=P) every partition key, public ones included, must be a "
+            f"dense id in [0, P)")
+
+
 def _device_bitmap(ids: torch.Tensor, P: int, device) -> Tuple[torch.Tensor, int]:
     """Bitmap of P bits (bit i of byte i >> 3 = partition i public) built on
-    the device, and the number of distinct in-range ids."""
-    ids = ids[(ids >= 0) & (ids < P)]
+    the device, and the number of distinct ids (all must lie in [0, P))."""
+    if ids.numel():
+        _check_public_range(*_range(ids), P)
     flags = torch.zeros(((P + 7) // 8) * 8, dtype=torch.uint8, device=device)
     flags[ids] = 1
     count = int(flags.sum(dtype=torch.int64).item())
@@ -257,7 +277,8 @@ def encode(col, extractors, device: torch.device, need_values: bool,
     elif public_ids is not None:
         mask = np.zeros((P + 7) // 8, dtype=np.uint8)
         ids = np.unique(np.asarray(public_ids, dtype=np.int64))
-        ids = ids[(ids >= 0) & (ids < P)]
+        if ids.size and key_table is None:
+            _check_public_range(int(ids[0]), int(ids[-1]), P)
         np.bitwise_or.at(mask, ids >> 3, (1 << (ids & 7)).astype(np.uint8))
         enc.public_mask = torch.from_numpy(mask).to(device)
         enc.public_count = int(ids.size)

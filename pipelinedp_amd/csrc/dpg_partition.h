@@ -642,34 +642,6 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
         __syncthreads();
         const uint32_t total =
             scatter_scan_update<kScatThreads, FMAX / kScatThreads>(cnt, dstart, cur, F, sh16);
-#ifdef DPG_SCAT_DIRECT
-        // experiment: every thread writes its own records straight to their
-        // final positions (no LDS staging; stores not coalesced by digit)
-        {
-            uint32_t c1[IPT], c2[IPT], c3[IPT];
-#pragma unroll
-            for (int j = 0; j < IPT; ++j) {
-                const uint32_t d = dr[j] != ~0u ? (dr[j] & 0xFFFu) : 0u;
-                c1[j] = cur[d];
-                c2[j] = dstart[d + 1];
-                c3[j] = dstart[d];
-            }
-#pragma unroll
-            for (int j = 0; j < IPT; ++j)
-                if (dr[j] != ~0u)
-                    *reinterpret_cast<W *>(&out[c1[j] - c2[j] + c3[j] + (dr[j] >> 12)]) =
-                        to_words(rec[j]);
-            __syncthreads();
-            const int64_t nb = sb + SUB;
-            const uint32_t nlim = (uint32_t)max<int64_t>(0, min<int64_t>(SUB, td.end - nb));
-            if (nlim > 0) {
-#pragma unroll
-                for (int j = 0; j < IPT; ++j)
-                    raw[j] = src.fetch(nb + min((uint32_t)(j * kScatThreads + tid), nlim - 1));
-            }
-            continue;
-        }
-#endif
         {
             uint32_t ds[IPT];
 #pragma unroll
@@ -715,15 +687,8 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
             // cur already includes this sub-tile: its run ends at cur[d]
             // (non-temporal loads / stores measured slower: the partial
             // lines of the runs merge in L2)
-#ifdef DPG_SCAT_LINEAR
-            // timing experiment only (wrong output): contiguous writes
-#pragma unroll
-            for (int u = 0; u < WB; ++u)
-                *reinterpret_cast<W *>(&out[(uint32_t)(sb - td.begin) + (uint32_t)td.begin + kc[u] + 0u * (c1[u] - c2[u])]) = x[u];
-#else
 #pragma unroll
             for (int u = 0; u < WB; ++u) *reinterpret_cast<W *>(&out[c1[u] - c2[u] + kc[u]]) = x[u];
-#endif
         }
         // the next sub-tile's first barrier (after its ranking) orders this
         // write-out's LDS reads before the next scan and staging

@@ -1,5 +1,6 @@
 """Ingest: dictionary encoding of partition keys / privacy ids (CPU tensors)."""
 import numpy as np
+import pytest
 import torch
 
 import pipelinedp_amd as pdp
@@ -47,15 +48,41 @@ def test_public_bitmap_from_range_array_and_tensor_matches_list():
     col = pdp.ColumnarData(pid=np.array([1, 2]), pk=np.array([2, 40]), value=np.array([0.0, 1.0]),
                            n_partitions=45)
     ex = pdp.DataExtractors("pid", "pk", "value")
-    ids = [0, 3, 8, 9, 17, 40, 44, 44, 50, -1]  # duplicates and out-of-range ids
+    ids = [0, 3, 8, 9, 17, 40, 44, 44, 9]  # duplicates
     ref = columnar.encode(col, ex, CPU, True, public_partitions=ids)
     for pub in (np.array(ids), torch.tensor(ids), range(0, 45, 3)):
         enc = columnar.encode(col, ex, CPU, True, public_partitions=pub)
         if isinstance(pub, range):
             want = list(pub)
         else:
-            want = sorted({i for i in ids if 0 <= i < 45})
+            want = sorted(set(ids))
             assert torch.equal(enc.public_mask, ref.public_mask)
         bits = np.unpackbits(enc.public_mask.numpy(), bitorder="little")[:45]
         assert np.nonzero(bits)[0].tolist() == want
         assert enc.public_count == len(want)
+
+
+def test_public_ids_outside_declared_range_raise():
+    # with n_partitions=P every key is a dense id in [0, P); a public id
+    # outside that range cannot be represented and is an error, not a drop
+    col = pdp.ColumnarData(pid=np.array([1, 2]), pk=np.array([2, 40]), value=np.array([0.0, 1.0]),
+                           n_partitions=45)
+    ex = pdp.DataExtractors("pid", "pk", "value")
+    for pub in ([0, 50], np.array([3, -1]), torch.tensor([45]), range(0, 46)):
+        with pytest.raises(ValueError, match="outside"):
+            columnar.encode(col, ex, CPU, True, public_partitions=pub)
+
+
+def test_integer_data_keys_with_non_integer_public_partitions():
+    # reference semantics: public partitions are arbitrary hashable keys; the
+    # ones that never occur in the data are released as empty partitions
+    col = pdp.ColumnarData(pid=torch.arange(6), pk=torch.tensor([5, 5, 7, 7, 10**12, 10**12]),
+                           value=torch.ones(6))
+    enc = columnar.encode(col, pdp.DataExtractors("pid", "pk", "value"), CPU, True,
+                          public_partitions=[5, "x", 7])
+    keys = columnar.decode_keys(np.arange(enc.n_partitions), enc.key_table)
+    assert sorted(map(str, keys)) == sorted(["5", "7", str(10**12), "x"])
+    assert [keys[i] for i in enc.pk.tolist()] == [5, 5, 7, 7, 10**12, 10**12]
+    bits = np.unpackbits(enc.public_mask.numpy(), bitorder="little")[:enc.n_partitions]
+    assert sorted(str(keys[i]) for i in np.nonzero(bits)[0]) == ["5", "7", "x"]
+    assert enc.public_count == 3
