@@ -276,8 +276,11 @@ int run_level(dpg_ctx *ctx, hipStream_t s, const Src &src, uint32_t S, const int
 // record; later levels recompute it
 template <class R>
 struct Ipt {
-    static constexpr int L1 = sizeof(R) == 8 ? 12 : 6;
-    static constexpr int LN = sizeof(R) == 8 ? 16 : 8;
+    static constexpr int L1 = sizeof(R) == 8 ? 12 : 8;
+    static constexpr int LN = sizeof(R) == 8 ? 16 : 10;
+    // the refine level has few digits (wave-aggregated ranking, which holds
+    // more registers per record: at LN records per thread it spilled)
+    static constexpr int LR = sizeof(R) == 8 ? 8 : 6;
 };
 
 BoundParams to_bound(const dpg_bound_params *p, uint64_t seed) {
@@ -380,7 +383,7 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
             uint32_t *tot2;
             const uint32_t shift = pl.pkbits + (pl.kbits - pl.b1) - pl.b2 - rbits;
             SrcAoS<R> src{recs, f, shift, F2 - 1};
-            int r = run_level<SrcAoS<R>, R, Ipt<R>::LN, 2048>(ctx, s, src, no, ostart, ocnt,
+            int r = run_level<SrcAoS<R>, R, Ipt<R>::LR, 2048>(ctx, s, src, no, ostart, ocnt,
                                                                nullptr, acc, F2, rbits, rbuf,
                                                                "refine", &base2, &tot2,
                                                                &ctl->ntiles[3], oout);
@@ -811,7 +814,7 @@ int aggregate_impl(dpg_ctx *ctx, const int64_t *pid, const int64_t *pk, const do
     const uint32_t ib = std::max<uint32_t>(1, bits_for((uint64_t)n));
     const bool r8 = (pl.kbits - pl.b1) + pl.pkbits + ib <= 64;
     if (r8) return pipeline<R8>(ctx, s, pid, pk, value, n, p, out, ctl, pl, pid_min, U, ib, pa);
-    return pipeline<R16>(ctx, s, pid, pk, value, n, p, out, ctl, pl, pid_min, U, ib, pa);
+    return pipeline<R12>(ctx, s, pid, pk, value, n, p, out, ctl, pl, pid_min, U, ib, pa);
 }
 
 }  // namespace

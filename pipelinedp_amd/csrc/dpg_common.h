@@ -23,14 +23,13 @@ namespace dpg {
 // bits; the stored key drops the level-1 digit (the top b1 bits of h), which
 // the bucket position implies.
 //   R8 : one word, stored_key << ib | idx    (when it fits 64 bits)
-//   R16: stored_key, idx                      (always fits)
+//   R12: stored_key (two words), idx          (always fits; 12 bytes, so
+//        the wide format moves 3/4 of the bytes a padded 16-byte record would)
 struct alignas(8) R8 {
     uint64_t w;
 };
-struct alignas(16) R16 {
-    uint64_t key;
-    uint32_t idx;
-    uint32_t pad;
+struct alignas(4) R12 {
+    uint32_t lo, hi, idx;
 };
 
 struct Fmt {
@@ -55,15 +54,15 @@ struct RecOps<R8> {
     }
 };
 template <>
-struct RecOps<R16> {
-    static __host__ __device__ __forceinline__ uint64_t key(const R16 &r, const Fmt &) {
-        return r.key;
+struct RecOps<R12> {
+    static __host__ __device__ __forceinline__ uint64_t key(const R12 &r, const Fmt &) {
+        return ((uint64_t)r.hi << 32) | r.lo;
     }
-    static __host__ __device__ __forceinline__ uint32_t idx(const R16 &r, const Fmt &) {
+    static __host__ __device__ __forceinline__ uint32_t idx(const R12 &r, const Fmt &) {
         return r.idx;
     }
-    static __host__ __device__ __forceinline__ R16 make(uint64_t key, uint32_t idx, const Fmt &) {
-        return R16{key, idx, 0u};
+    static __host__ __device__ __forceinline__ R12 make(uint64_t key, uint32_t idx, const Fmt &) {
+        return R12{(uint32_t)key, (uint32_t)(key >> 32), idx};
     }
 };
 

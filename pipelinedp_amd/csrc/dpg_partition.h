@@ -23,7 +23,7 @@ namespace dpg {
 #define DPG_HIST_U 8
 #endif
 #ifndef DPG_SCAT_WB
-#define DPG_SCAT_WB 8
+#define DPG_SCAT_WB 4  // same-box A/B: 8 -> 4 level-1 scatter 7.51 -> 7.45 ms (fewer live registers)
 #endif
 constexpr int kPartThreads = 1024;  // 16 waves
 // scatter workgroups (512 threads with twice the records per thread measured
@@ -46,8 +46,13 @@ struct TileDesc {
 template <class R>
 struct SrcSoAKey {
     static constexpr bool kDigitFromRec = false;
+    // the scatter loads only the low word of the privacy id: the digit and
+    // the stored key depend on (pid - pid_min) mod 2^32 alone, and the
+    // histogram pass, which reads the whole column, raises the range error
+    // (12 fewer VGPRs per thread in flight: the level-1 scatter spilled)
     struct Raw {
-        int64_t pid, pk;
+        uint32_t pid;
+        int64_t pk;
     };
     const int64_t *pid;
     const int64_t *pk;
@@ -67,30 +72,39 @@ struct SrcSoAKey {
     // the key columns are read once: non-temporal loads leave L2 to the
     // scattered runs being written
     __device__ __forceinline__ Raw fetch(int64_t i) const {
-        return Raw{__builtin_nontemporal_load(pid + i), __builtin_nontemporal_load(pk + i)};
+        return Raw{__builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(pid) + 2 * i),
+                   __builtin_nontemporal_load(pk + i)};
     }
 #else
-    __device__ __forceinline__ Raw fetch(int64_t i) const { return Raw{pid[i], pk[i]}; }
+    __device__ __forceinline__ Raw fetch(int64_t i) const {
+        return Raw{reinterpret_cast<const uint32_t *>(pid)[2 * i], pk[i]};
+    }
 #endif
+    // keep decision shared by the histogram and the scatter (they must agree
+    // record for record): from the low word of pid - pid_min and pk
+    __device__ __forceinline__ bool keep(uint32_t a, int64_t b) const {
+        if (!pub) return true;
+        const bool in_range = (uint64_t)a < U && (uint64_t)b < (uint64_t)P;
+        return !(in_range && !((pub[b >> 3] >> (b & 7)) & 1));
+    }
     __device__ __forceinline__ bool decode(const Raw &x, int64_t i, R &r, uint32_t &d) const {
-        const uint64_t a = (uint64_t)(x.pid - pid_min);
-        const bool in_range = a < U && (uint64_t)x.pk < (uint64_t)P;
-        if (!in_range) atomicOr(err, 1u);
-        const uint32_t h = hk((uint32_t)a, H);
+        const uint32_t a = x.pid - (uint32_t)pid_min;
+        if ((uint64_t)x.pk >= (uint64_t)P) atomicOr(err, 1u);
+        const uint32_t h = hk(a, H);
         d = h >> dshift;
         const uint64_t key = (((uint64_t)h << f.pkbits) | (uint64_t)x.pk) & kmask;
         r = RecOps<R>::make(key, (uint32_t)i, f);
-        return !(pub && in_range && !((pub[x.pk >> 3] >> (x.pk & 7)) & 1));
+        return keep(a, x.pk);
     }
     // histogram view: the same digit and keep decision from pid (and pk
-    // only when a public-partition filter applies)
+    // only when a public-partition filter applies); the privacy-id range
+    // check of the whole 64-bit id
     __device__ __forceinline__ bool hist(int64_t i, uint32_t &d) const {
         const uint64_t a = (uint64_t)(pid[i] - pid_min);
+        if (a >= U) atomicOr(err, 1u);
         d = hk((uint32_t)a, H) >> dshift;
         if (!pub) return true;
-        const int64_t b = pk[i];
-        const bool in_range = a < U && (uint64_t)b < (uint64_t)P;
-        return !(in_range && !((pub[b >> 3] >> (b & 7)) & 1));
+        return keep((uint32_t)a, pk[i]);
     }
 };
 
@@ -494,17 +508,22 @@ __device__ __forceinline__ uint32_t wave_agg_rank(uint32_t *cnt, uint32_t d, boo
     return basev + below;
 }
 
-// Records travel through registers and LDS as raw 8- or 16-byte words
+// Records travel through registers and LDS as raw 16-, 8- or 4-byte words
 // (struct copies would be demoted to scratch by the compiler).
-template <class T, bool kQuad = (sizeof(T) % 16 == 0)>
+template <class T, int kW = (sizeof(T) % 16 == 0 ? 16 : sizeof(T) % 8 == 0 ? 8 : 4)>
 struct Words {
     static constexpr int N = sizeof(T) / 16;
     uint4 w[N];
 };
 template <class T>
-struct Words<T, false> {
+struct Words<T, 8> {
     static constexpr int N = sizeof(T) / 8;
     uint2 w[N];
+};
+template <class T>
+struct Words<T, 4> {
+    static constexpr int N = sizeof(T) / 4;
+    uint32_t w[N];
 };
 template <class T>
 __device__ __forceinline__ Words<T> to_words(const T &r) {

@@ -47,15 +47,25 @@ __global__ __launch_bounds__(1024) void k_reduce_items(const Item *items, const 
         s_cnt[k] = 0;
     }
     __syncthreads();
-    for (int64_t i = td.begin + tid; i < td.end; i += 1024) {
-        Item it = items[i];
-        uint32_t k = it.pk & (kRange - 1);
-        atomicAdd(&s_rows[k], 1u);
-        atomicAdd(&s_cnt[k], it.cnt);
-        if (it.sum != 0.0) atomicAdd(&s_sum[k], it.sum);
-        if constexpr (kVar) {
-            if (it.nsum != 0.0) atomicAdd(&s_nsum[k], it.nsum);
-            if (it.nsq != 0.0) atomicAdd(&s_nsq[k], it.nsq);
+    // kRU item loads per thread in flight before their LDS atomics (one
+    // outstanding load per thread left the kernel latency-bound); items past
+    // the tile end add nothing
+    constexpr int kRU = sizeof(Item) <= 16 ? 8 : 4;
+    for (int64_t i0 = td.begin; i0 < td.end; i0 += (int64_t)kRU * 1024) {
+        Item it[kRU];
+#pragma unroll
+        for (int u = 0; u < kRU; ++u) it[u] = items[min(i0 + u * 1024 + tid, td.end - 1)];
+#pragma unroll
+        for (int u = 0; u < kRU; ++u) {
+            if (i0 + u * 1024 + tid >= td.end) continue;
+            const uint32_t k = it[u].pk & (kRange - 1);
+            atomicAdd(&s_rows[k], 1u);
+            atomicAdd(&s_cnt[k], it[u].cnt);
+            if (it[u].sum != 0.0) atomicAdd(&s_sum[k], it[u].sum);
+            if constexpr (kVar) {
+                if (it[u].nsum != 0.0) atomicAdd(&s_nsum[k], it[u].nsum);
+                if (it[u].nsq != 0.0) atomicAdd(&s_nsq[k], it[u].nsq);
+            }
         }
     }
     __syncthreads();

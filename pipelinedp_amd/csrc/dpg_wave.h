@@ -72,6 +72,11 @@ struct WaveLayout {
 #ifndef DPG_RT_W
 #define DPG_RT_W 8
 #endif
+// same-box A/B, config 2: late gathers cut the value traffic of the
+// bounding kernel but cost 13.0 -> 13.75 ms (their latency is exposed)
+#ifndef DPG_LATE_GATHER
+#define DPG_LATE_GATHER 0
+#endif
 // candidate bounds: round-0 mpc candidates ~ k + E0 sqrt(k) + E0 per pid,
 // pre-filter ~ CAND x (k + 2 sqrt(k) + 2) records per pid (same-box A/B,
 // config 2 / config 4 bound ms: (2.0, 2.0) 14.2 / 31.7; (1.5, 1.25) 13.1 /
@@ -726,7 +731,12 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
             if (st[k] < kKeptAll) st[k] &= 0xFFFFu;  // base (appends in the high bits)
             v[k] = 0.0;
             rkey[k] = 0;
-            if (need_v && st[k] != kDropped) v[k] = bp.value[RecOps<R>::idx(cur[k], f)];
+            // values of records whose pair keeps every record load now; the
+            // records of over-full pairs load once their sample is known
+            // (DPG_LATE_GATHER: most of them are not kept, and every gather
+            // pulls a whole sector)
+            if (need_v && (DPG_LATE_GATHER ? st[k] == kKeptAll : st[k] != kDropped))
+                v[k] = bp.value[RecOps<R>::idx(cur[k], f)];
         }
         if (sample) {
             uint32_t pv[kWRPT], pos[kWRPT];
@@ -768,6 +778,11 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
 #pragma unroll
                 for (int k = 0; k < kWRPT && k < (int)kn; ++k)
                     if (st[k] < kKeptAll && rkey[k] <= thr[k]) keepm |= 1u << k;
+#if DPG_LATE_GATHER
+#pragma unroll
+                for (int k = 0; k < kWRPT && k < (int)kn; ++k)
+                    if (st[k] < kKeptAll && rkey[k] <= thr[k]) v[k] = bp.value[RecOps<R>::idx(cur[k], f)];
+#endif
             }
 #pragma unroll
             for (int k = 0; k < kWRPT && k < (int)kn; ++k) {
