@@ -454,7 +454,14 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&wpc, wave_kern, 64, WL::TOTAL) != hipSuccess ||
         wpc <= 0)
         wpc = 1;
-    const uint32_t Gw = (uint32_t)(ctx->n_cu * std::min(wpc, WL::PER_CU));
+    // waves per CU rounded down to a multiple of the 4 SIMDs: the static
+    // schedule gives every wave the same share of chunks, so two waves
+    // sharing a SIMD next to SIMDs with one would finish last (same-box
+    // A/B, config 4 with 32-KB working sets: 5 waves per CU 42 ms, 4 per
+    // CU 29.7 ms)
+    int per_cu = std::min(wpc, WL::PER_CU);
+    if (per_cu > 4) per_cu &= ~3;
+    const uint32_t Gw = (uint32_t)(ctx->n_cu * per_cu);
     const uint32_t Gm = hctl.n_mchunks ? (uint32_t)std::min<uint32_t>(
                                              ctx->n_cu * CL::PER_CU, hctl.n_mchunks)
                                        : 0u;
@@ -674,7 +681,8 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
         k_build_tiles<<<(F + 255) / 256, 256, 0, s>>>(baseR, totR, nullptr, F, rtile, rt, rstb,
                                                       rsnt, &ctl->ntiles[5]);
         LAUNCH_CHECK();
-        size_t lds_r = (size_t)kRange * (ItemTraits<Item>::var ? 3 * 8 : 8) + kRange * 8;
+        size_t lds_r = (size_t)kRange * 8 * (ItemTraits<Item>::var ? (ItemTraits<Item>::sum ? 3 : 2) : 1) +
+                       kRange * 8;
         k_reduce_items<Item><<<max_tiles, 1024, lds_r, s>>>(sorted, rt, &ctl->ntiles[5], P, po);
         LAUNCH_CHECK();
     }
@@ -740,6 +748,13 @@ int pipeline(dpg_ctx *ctx, hipStream_t s, const int64_t *pid, const int64_t *pk,
                                                              n, out, ctl, pa)
                      : bound_and_reduce<R, uint64_t, ItemPA>(ctx, s, pl, cur, bstart, bcnt, B, bp,
                                                              n, out, ctl, pa);
+    // MEAN / VARIANCE without SUM (and without per-partition sum clipping):
+    // 24-byte items with the normalised moments only
+    if (var && !(p->metric_mask & DPG_M_SUM) && p->sum_mode != DPG_SUM_CLIP_PARTITION)
+        return key32 ? bound_and_reduce<R, uint32_t, ItemV>(ctx, s, pl, cur, bstart, bcnt, B, bp,
+                                                            n, out, ctl, nullptr)
+                     : bound_and_reduce<R, uint64_t, ItemV>(ctx, s, pl, cur, bstart, bcnt, B, bp,
+                                                            n, out, ctl, nullptr);
     if (var)
         return key32 ? bound_and_reduce<R, uint32_t, Item32>(ctx, s, pl, cur, bstart, bcnt, B, bp,
                                                              n, out, ctl, nullptr)

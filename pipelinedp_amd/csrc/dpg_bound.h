@@ -113,15 +113,25 @@ __host__ __device__ __forceinline__ size_t align16(size_t x) { return (x + 15) &
 
 template <class Item>
 struct ItemTraits;
+// sum: the item carries the clipped sum (MEAN / VARIANCE without SUM need
+// only the normalised moments: 24-byte items and one accumulator less)
 template <>
 struct ItemTraits<Item16> {
     static constexpr bool var = false;
     static constexpr bool preagg = false;
+    static constexpr bool sum = true;
 };
 template <>
 struct ItemTraits<Item32> {
     static constexpr bool var = true;
     static constexpr bool preagg = false;
+    static constexpr bool sum = true;
+};
+template <>
+struct ItemTraits<ItemV> {
+    static constexpr bool var = true;
+    static constexpr bool preagg = false;
+    static constexpr bool sum = false;
 };
 // utility-analysis pre-aggregate: every pair kept (the host passes no-op
 // bounds), each pair also carries its privacy id's partition and record
@@ -130,6 +140,7 @@ template <>
 struct ItemTraits<ItemPA> {
     static constexpr bool var = false;
     static constexpr bool preagg = true;
+    static constexpr bool sum = true;
 };
 
 __device__ __forceinline__ uint32_t hslot(uint32_t key, uint32_t mask) {
@@ -526,7 +537,7 @@ __global__ __launch_bounds__(kBigThreads) void k_bound_big(
             s = acc_sum[p];
             if (part_clip) s = clampd(s, bp.lo_pp, bp.hi_pp);
         }
-        it.sum = s;
+        if constexpr (ItemTraits<Item>::sum) it.sum = s;
         if constexpr (kVar) {
             it.nsum = need_v ? acc_nsum[p] : 0.0;
             it.nsq = need_v ? acc_nsq[p] : 0.0;

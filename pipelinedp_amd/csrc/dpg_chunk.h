@@ -527,7 +527,7 @@ __device__ __forceinline__ void bound_chunk(const R (&r)[kRPT], uint32_t n, uint
             s = acc_sum[p];
             if (part_clip) s = clampd(s, bp.lo_pp, bp.hi_pp);
         }
-        it.sum = s;
+        if constexpr (ItemTraits<Item>::sum) it.sum = s;
         if constexpr (kVar) {
             it.nsum = need_v ? acc_nsum[p] : 0.0;
             it.nsq = need_v ? acc_nsq[p] : 0.0;

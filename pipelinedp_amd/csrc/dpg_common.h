@@ -80,6 +80,13 @@ struct alignas(16) Item32 {  // one kept pair with MEAN / VARIANCE moments
     double nsq;
 };
 
+struct alignas(8) ItemV {  // one kept pair with MEAN / VARIANCE moments, no SUM requested
+    uint32_t pk;
+    uint32_t cnt;
+    double nsum;
+    double nsq;
+};
+
 struct alignas(16) ItemPA {  // one (pid, pk) pair of the utility-analysis pre-aggregate
     uint32_t pk;
     uint32_t cnt;       // records of the pair

@@ -27,18 +27,20 @@ __global__ __launch_bounds__(1024) void k_reduce_items(const Item *items, const 
                                                        const uint32_t *ntiles, int64_t P,
                                                        Partials out) {
     constexpr bool kVar = ItemTraits<Item>::var;
+    constexpr bool kSum = ItemTraits<Item>::sum;
+    constexpr int kArr = kVar ? (kSum ? 3 : 2) : 1;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     double *s_sum = reinterpret_cast<double *>(smem);
-    double *s_nsum = s_sum + kRange;
+    double *s_nsum = s_sum + (kSum ? kRange : 0);
     double *s_nsq = s_nsum + kRange;
-    uint32_t *s_rows = reinterpret_cast<uint32_t *>(smem + (kVar ? 3 : 1) * kRange * 8);
+    uint32_t *s_rows = reinterpret_cast<uint32_t *>(smem + kArr * kRange * 8);
     uint32_t *s_cnt = s_rows + kRange;
     const uint32_t t = blockIdx.x;
     if (t >= *ntiles) return;
     const TileDesc td = tiles[t];
     const int tid = threadIdx.x;
     for (int k = tid; k < kRange; k += 1024) {
-        s_sum[k] = 0.0;
+        if (kSum) s_sum[k] = 0.0;
         if (kVar) {
             s_nsum[k] = 0.0;
             s_nsq[k] = 0.0;
@@ -61,7 +63,8 @@ __global__ __launch_bounds__(1024) void k_reduce_items(const Item *items, const 
             const uint32_t k = it[u].pk & (kRange - 1);
             atomicAdd(&s_rows[k], 1u);
             atomicAdd(&s_cnt[k], it[u].cnt);
-            if (it[u].sum != 0.0) atomicAdd(&s_sum[k], it[u].sum);
+            if constexpr (kSum)
+                if (it[u].sum != 0.0) atomicAdd(&s_sum[k], it[u].sum);
             if constexpr (kVar) {
                 if (it[u].nsum != 0.0) atomicAdd(&s_nsum[k], it[u].nsum);
                 if (it[u].nsq != 0.0) atomicAdd(&s_nsq[k], it[u].nsq);
@@ -75,7 +78,7 @@ __global__ __launch_bounds__(1024) void k_reduce_items(const Item *items, const 
         if (pk >= P || s_rows[k] == 0) continue;
         atomicAdd((unsigned long long *)&out.rows[pk], (unsigned long long)s_rows[k]);
         atomicAdd((unsigned long long *)&out.count[pk], (unsigned long long)s_cnt[k]);
-        if (out.sum) atomicAdd(&out.sum[pk], s_sum[k]);
+        if (kSum && out.sum) atomicAdd(&out.sum[pk], s_sum[k]);
         if constexpr (kVar) {
             if (out.nsum) atomicAdd(&out.nsum[pk], s_nsum[k]);
             if (out.nsq) atomicAdd(&out.nsq[pk], s_nsq[k]);
@@ -93,7 +96,8 @@ __global__ void k_reduce_items_direct(Src items, const uint32_t *n_items, Partia
         const Item it = src.fetch(i);
         atomicAdd((unsigned long long *)&out.rows[it.pk], 1ull);
         atomicAdd((unsigned long long *)&out.count[it.pk], (unsigned long long)it.cnt);
-        if (out.sum) atomicAdd(&out.sum[it.pk], it.sum);
+        if constexpr (ItemTraits<Item>::sum)
+            if (out.sum) atomicAdd(&out.sum[it.pk], it.sum);
         if constexpr (kVar) {
             if (out.nsum) atomicAdd(&out.nsum[it.pk], it.nsum);
             if (out.nsq) atomicAdd(&out.nsq[it.pk], it.nsq);

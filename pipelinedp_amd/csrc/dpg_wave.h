@@ -59,7 +59,7 @@ struct WaveLayout {
     static constexpr size_t PST = PCNT + 4 * kWCp;              // dense: state
     static constexpr size_t POOL = PST + 4 * kWCp;
     static constexpr size_t ACC = POOL + 8 * kWPool;
-    static constexpr size_t END = ACC + 8 * kWCp * (var ? 3 : 1);
+    static constexpr size_t END = ACC + 8 * kWCp * (var ? (ItemTraits<Item>::sum ? 3 : 2) : 1);
     // padded to a multiple of 4 KB so that the allocation granularity of LDS
     // cannot cost a resident wave (20 KB: 8 per CU)
     static constexpr size_t TOTAL = (END + 4095) & ~(size_t)4095;
@@ -255,6 +255,7 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
                                                uint32_t hbound = 0, uint32_t hidx = 0) {
     using L = WaveLayout<KeyT, Item>;
     constexpr bool kVar = L::var;
+    constexpr bool kSum = ItemTraits<Item>::sum;  // false: MEAN / VARIANCE moments only
     uint32_t *pidv = reinterpret_cast<uint32_t *>(smem + L::PIDV);
     uint32_t *pidm = reinterpret_cast<uint32_t *>(smem + L::PIDM);
     uint32_t *pidslot = reinterpret_cast<uint32_t *>(smem + L::PIDSLOT);
@@ -264,7 +265,7 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
     uint32_t *pst = reinterpret_cast<uint32_t *>(smem + L::PST);
     uint64_t *pool = reinterpret_cast<uint64_t *>(smem + L::POOL);
     double *acc_sum = reinterpret_cast<double *>(smem + L::ACC);
-    double *acc_nsum = acc_sum + kWCp;
+    double *acc_nsum = acc_sum + (kSum ? kWCp : 0);
     double *acc_nsq = acc_nsum + kWCp;
 
     const uint32_t lane = __lane_id();
@@ -497,7 +498,7 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
                 pkey_d[d] = pkey[k];
                 pcnt[d] = 0;
                 if (need_v) {
-                    acc_sum[d] = 0.0;
+                    if (kSum) acc_sum[d] = 0.0;
                     if (kVar) {
                         acc_nsum[d] = 0.0;
                         acc_nsq[d] = 0.0;
@@ -792,7 +793,7 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
                     atomicAdd(&acc_sum[p], v[k]);
                 } else {
                     const double x = clampd(v[k], bp.lo, bp.hi);
-                    atomicAdd(&acc_sum[p], x);
+                    if (kSum) atomicAdd(&acc_sum[p], x);
                     if (kVar) {
                         const double y = x - bp.mid;
                         atomicAdd(&acc_nsum[p], y);
@@ -864,7 +865,7 @@ bool overp[kWQPL];
                     atomicAdd(&acc_sum[p], v[k]);
                 } else {
                     const double x = clampd(v[k], bp.lo, bp.hi);
-                    atomicAdd(&acc_sum[p], x);
+                    if (kSum) atomicAdd(&acc_sum[p], x);
                     if (kVar) {
                         const double y = x - bp.mid;
                         atomicAdd(&acc_nsum[p], y);
@@ -901,7 +902,7 @@ bool overp[kWQPL];
 #pragma unroll
         for (int j = 0; j < kWPPL && j < (int)jn; ++j) {
             const uint32_t d = lane + 64u * j;
-            a0[j] = need_v ? acc_sum[d] : 0.0;
+            a0[j] = (kSum && need_v) ? acc_sum[d] : 0.0;
             if constexpr (kVar) {
                 a1[j] = need_v ? acc_nsum[d] : 0.0;
                 a2[j] = need_v ? acc_nsq[d] : 0.0;
@@ -915,7 +916,8 @@ bool overp[kWQPL];
                 Item it;
                 it.pk = (uint32_t)(pkv[j] & (KeyT)pkmask);
                 it.cnt = ecnt[j];
-                it.sum = (need_v && part_clip) ? clampd(a0[j], bp.lo_pp, bp.hi_pp) : a0[j];
+                if constexpr (kSum)
+                    it.sum = (need_v && part_clip) ? clampd(a0[j], bp.lo_pp, bp.hi_pp) : a0[j];
                 if constexpr (kVar) {
                     it.nsum = a1[j];
                     it.nsq = a2[j];
