@@ -37,7 +37,9 @@ using namespace dpg;
 namespace {
 
 constexpr uint32_t kBucketTarget = 256;  // average records per fine bucket
-constexpr uint32_t kMaxB1 = 11, kMaxB2 = 11;
+// level 2 (records) may take 12 bits (4096 digits: its scatter stages fewer
+// records per sub-tile); refine and item levels keep <= 11
+constexpr uint32_t kMaxB1 = 11, kMaxB2 = 12, kMaxBR = 11;
 constexpr uint32_t kChunkGroup = 32;     // fine buckets per packing thread
 
 struct Buf {
@@ -240,6 +242,9 @@ int run_level(dpg_ctx *ctx, hipStream_t s, const Src &src, uint32_t S, const int
                                                       stb, snt, ntiles_dev, xq);
     }
     LAUNCH_CHECK();
+    if (F > 2048)
+        (void)hipFuncSetAttribute((const void *)k_hist<Src>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)(4 * F * sizeof(uint32_t)));
     k_hist<Src><<<max_tiles, kPartThreads, 4 * F * sizeof(uint32_t), s>>>(src, tiles, ntiles_dev,
                                                                           F, hist);
     LAUNCH_CHECK();
@@ -281,6 +286,8 @@ struct Ipt {
     // the refine level has few digits (wave-aggregated ranking, which holds
     // more registers per record: at LN records per thread it spilled)
     static constexpr int LR = sizeof(R) == 8 ? 8 : 6;
+    // level 2 with 4096 digits: the digit arrays take 48 KB of LDS
+    static constexpr int LW = sizeof(R) == 8 ? 12 : 8;
 };
 
 BoundParams to_bound(const dpg_bound_params *p, uint64_t seed) {
@@ -365,7 +372,7 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     const uint32_t *g_d1 = od1;
     uint32_t n_global = 0;
     if (hctl.n_over > 0) {
-        const uint32_t rbits = std::min<uint32_t>(kMaxB2, pl.plb);  // hash bits not yet used
+        const uint32_t rbits = std::min<uint32_t>(kMaxBR, pl.plb);  // hash bits not yet used
         if (rbits == 0) {
             n_global = hctl.n_over;
         } else {
@@ -619,7 +626,7 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     uint32_t F = 1;
     if (n_items > 0) {
         const uint32_t rb = std::max<uint32_t>(1, bits_for((uint64_t)std::max<int64_t>(1, nranges)));
-        const uint32_t b2 = rb > 10 ? std::min<uint32_t>(kMaxB2, rb - 1) : 0u;
+        const uint32_t b2 = rb > 10 ? std::min<uint32_t>(kMaxBR, rb - 1) : 0u;
         const uint32_t b1 = rb - b2;
         const uint32_t F1 = nranges <= 1024 ? (uint32_t)std::max<int64_t>(1, nranges) : 1u << b1;
         WS(items2, Item, "items2", n_items);
@@ -729,9 +736,15 @@ int pipeline(dpg_ctx *ctx, hipStream_t s, const int64_t *pid, const int64_t *pk,
 #ifndef DPG_L2_XCD
 #define DPG_L2_XCD 1
 #endif
-        r = run_level<SrcAoS<R>, R, Ipt<R>::LN, 2048>(ctx, s, s2, F1, bstart, bcnt, nullptr, n, F2,
-                                                       pl.b2, recB, "partition2", &bstart, &bcnt,
-                                                       &ctl->ntiles[1], nullptr, DPG_L2_XCD != 0);
+        r = pl.b2 > 11
+                ? run_level<SrcAoS<R>, R, Ipt<R>::LW, 4096>(ctx, s, s2, F1, bstart, bcnt, nullptr, n,
+                                                             F2, pl.b2, recB, "partition2", &bstart,
+                                                             &bcnt, &ctl->ntiles[1], nullptr,
+                                                             DPG_L2_XCD != 0)
+                : run_level<SrcAoS<R>, R, Ipt<R>::LN, 2048>(ctx, s, s2, F1, bstart, bcnt, nullptr, n,
+                                                             F2, pl.b2, recB, "partition2", &bstart,
+                                                             &bcnt, &ctl->ntiles[1], nullptr,
+                                                             DPG_L2_XCD != 0);
         if (r) return r;
         cur = recB;
         B = F1 * F2;

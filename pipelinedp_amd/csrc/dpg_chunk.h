@@ -41,7 +41,7 @@ constexpr int kWCap = DPG_WCAP;        // records per small chunk
 constexpr int kWRPT = kWCap / 64;      // records per lane
 constexpr uint32_t kWCq = 128;         // direct pid slots per small chunk
 constexpr uint32_t kWCp = kWCap;       // pairs (dense ids) per small chunk
-constexpr uint32_t kWCk = 1024;        // pair key table slots (load <= 1/2)
+constexpr uint32_t kWCk = 2 * kWCap;   // pair key table slots (load <= 1/2)
 constexpr uint32_t kWPool = kWCap;     // selection keys (mpc regions, then mcpp regions)
 constexpr int kWQPL = kWCq / 64;       // pid slots per lane
 constexpr int kWPPL = kWCp / 64;       // pair slots per lane

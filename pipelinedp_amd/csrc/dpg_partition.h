@@ -32,6 +32,19 @@ constexpr int kScatThreads = 1024;
 
 __host__ __device__ constexpr size_t a16(size_t x) { return (x + 15) & ~(size_t)15; }
 
+typedef int64_t i64x2 __attribute__((ext_vector_type(2)));
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+
+// Sources without a pair view (kPairs false) take the one-record loop.
+template <class Src, class = void>
+struct HasPairs {
+    static constexpr bool value = false;
+};
+template <class Src>
+struct HasPairs<Src, decltype((void)Src::kPairs)> {
+    static constexpr bool value = Src::kPairs;
+};
+
 struct TileDesc {
     int64_t begin, end;
     uint32_t seg;
@@ -106,6 +119,25 @@ struct SrcSoAKey {
         if (!pub) return true;
         return keep((uint32_t)a, pk[i]);
     }
+    // two consecutive records (i even) by 16-byte loads: the histogram pass
+    // streams at the 16-B/lane rate instead of the 8-B one
+    static constexpr bool kPairs = true;
+    __device__ __forceinline__ bool pairs_ok() const {
+        return ((uintptr_t)pid & 15) == 0 && (!pub || ((uintptr_t)pk & 15) == 0);
+    }
+    __device__ __forceinline__ void hist2(int64_t i, uint32_t (&d)[2], bool (&ok)[2]) const {
+        const i64x2 p = *reinterpret_cast<const i64x2 *>(pid + i);
+        const uint64_t a0 = (uint64_t)(p.x - pid_min), a1 = (uint64_t)(p.y - pid_min);
+        if (a0 >= U || a1 >= U) atomicOr(err, 1u);
+        d[0] = hk((uint32_t)a0, H) >> dshift;
+        d[1] = hk((uint32_t)a1, H) >> dshift;
+        ok[0] = ok[1] = true;
+        if (pub) {
+            const i64x2 q = *reinterpret_cast<const i64x2 *>(pk + i);
+            ok[0] = keep((uint32_t)a0, q.x);
+            ok[1] = keep((uint32_t)a1, q.y);
+        }
+    }
 };
 
 // Bucketed records; digit = bits [shift, shift + log2 F) of the stored key.
@@ -128,6 +160,17 @@ struct SrcAoS {
     __device__ __forceinline__ bool hist(int64_t i, uint32_t &d) const {
         d = digit(a[i]);
         return true;
+    }
+    // 8-byte records: pairs by 16-byte loads (see SrcSoAKey::hist2)
+    static constexpr bool kPairs = sizeof(R) == 8;
+    __device__ __forceinline__ bool pairs_ok() const { return ((uintptr_t)a & 15) == 0; }
+    __device__ __forceinline__ void hist2(int64_t i, uint32_t (&d)[2], bool (&ok)[2]) const {
+        if constexpr (sizeof(R) == 8) {
+            const u64x2 w = *reinterpret_cast<const u64x2 *>(a + i);
+            d[0] = digit(R{w.x});
+            d[1] = digit(R{w.y});
+        }
+        ok[0] = ok[1] = true;
     }
 };
 
@@ -273,8 +316,49 @@ __global__ __launch_bounds__(kPartThreads) void k_hist(Src src_in, const TileDes
     __syncthreads();
     uint32_t *my = lh + copy * F;
     Src src = src_in;  // per-thread copy (sources may cache lookup state)
-    int64_t i = td.begin + tid;
     constexpr int U = DPG_HIST_U;  // loads per thread in flight per round
+    if constexpr (HasPairs<Src>::value) {
+        if (src.pairs_ok()) {
+            // pairs (i even, 16-byte aligned): an odd first record alone,
+            // then U / 2 pair loads per thread in flight, a last odd record
+            int64_t b = td.begin;
+            const int64_t e = td.end;
+            if (b & 1) {
+                uint32_t d;
+                if (tid == 0 && b < e && src.hist(b, d)) atomicAdd(&my[d], 1u);
+                ++b;
+            }
+            constexpr int U2 = U / 2 > 0 ? U / 2 : 1;
+            int64_t i = b + 2 * tid;
+            for (; i + 2 * (U2 - 1) * kPartThreads + 1 < e; i += 2 * U2 * kPartThreads) {
+                uint32_t d[U2][2];
+                bool ok[U2][2];
+#pragma unroll
+                for (int u = 0; u < U2; ++u) src.hist2(i + 2 * u * kPartThreads, d[u], ok[u]);
+#pragma unroll
+                for (int u = 0; u < U2; ++u) {
+                    if (ok[u][0]) atomicAdd(&my[d[u][0]], 1u);
+                    if (ok[u][1]) atomicAdd(&my[d[u][1]], 1u);
+                }
+            }
+            for (; i + 1 < e; i += 2 * kPartThreads) {
+                uint32_t d[2];
+                bool ok[2];
+                src.hist2(i, d, ok);
+                if (ok[0]) atomicAdd(&my[d[0]], 1u);
+                if (ok[1]) atomicAdd(&my[d[1]], 1u);
+            }
+            if (i < e) {
+                uint32_t d;
+                if (src.hist(i, d)) atomicAdd(&my[d], 1u);
+            }
+            __syncthreads();
+            for (uint32_t d = tid; d < F; d += kPartThreads)
+                hist[(size_t)t * F + d] = lh[d] + lh[F + d] + lh[2 * F + d] + lh[3 * F + d];
+            return;
+        }
+    }
+    int64_t i = td.begin + tid;
     for (; i + (U - 1) * kPartThreads < td.end; i += U * kPartThreads) {
         uint32_t d[U];
         bool ok[U];
@@ -473,19 +557,26 @@ __device__ __forceinline__ uint32_t scatter_scan_update(uint32_t *cnt, uint32_t 
     return total;
 }
 
-// grid S: base[s][d] = seg_start[s] + exclusive_prefix_d(tot[s][.])  (F <= 2048)
+// grid S: base[s][d] = seg_start[s] + exclusive_prefix_d(tot[s][.])  (F <= 4096)
 __global__ __launch_bounds__(1024) void k_digit_base(const int64_t *seg_start, uint32_t F,
                                                      const uint32_t *tot, int64_t *base) {
     __shared__ uint32_t sh[16];
     const uint32_t s = blockIdx.x;
-    const uint32_t d0 = 2 * threadIdx.x;
-    const uint32_t c0 = d0 < F ? tot[(size_t)s * F + d0] : 0u;
-    const uint32_t c1 = d0 + 1 < F ? tot[(size_t)s * F + d0 + 1] : 0u;
+    const uint32_t d0 = 4 * threadIdx.x;
+    uint32_t c[4], x = 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        c[u] = d0 + u < F ? tot[(size_t)s * F + d0 + u] : 0u;
+        x += c[u];
+    }
     uint32_t total;
-    const uint32_t e = block_excl_scan_1024(c0 + c1, sh, total);
+    uint32_t e = block_excl_scan_1024(x, sh, total);
     const int64_t st = seg_start ? seg_start[s] : 0;
-    if (d0 < F) base[(size_t)s * F + d0] = st + e;
-    if (d0 + 1 < F) base[(size_t)s * F + d0 + 1] = st + e + c0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        if (d0 + u < F) base[(size_t)s * F + d0 + u] = st + e;
+        e += c[u];
+    }
 }
 
 // ---------------------------------------------------------------- scatter

@@ -186,7 +186,11 @@ class DeviceAggregation:
             bound.nonce = nonce
             self.last_bound_fields = dict(bfields, pid_min=enc.pid_min, pid_count=enc.pid_count,
                                           rec_id_offset=enc.rec_id_offset, nonce=nonce)
-            if enc.public_mask is not None and self.drop_non_public:
+            # _drop_partitions (dp_engine.py:280-286) in the level-1 pass; a
+            # public set that covers every partition id drops nothing, so
+            # the per-record bitmap lookups are skipped
+            if (enc.public_mask is not None and self.drop_non_public
+                    and enc.public_count < enc.n_partitions):
                 bound.public_mask = enc.public_mask.data_ptr()
             partials = _native.Partials(P, rows.data_ptr(), count.data_ptr(),
                                         sum_.data_ptr() if sum_ is not None else None,

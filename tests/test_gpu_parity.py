@@ -150,6 +150,26 @@ def test_gpu_partition_levels_and_fallback(built, target, cap):
     assert np.allclose(got["sum"], ref["sum"], rtol=1e-9, atol=1e-9)
 
 
+def test_gpu_4096_digit_level(built, monkeypatch):
+    """A 12-bit second partition level (4096 digits: the scatter variant
+    with 48 KB of digit arrays, 4 digits per thread in the digit bases),
+    forced by the level-split hook: partials equal the oracle's."""
+    monkeypatch.setenv("DPG_DEBUG_B1", "1")
+    P = 3000
+    pid, pk, val = _dataset(23, 2_000_000, 1 << 20, P, zipf=1.1)
+    params = pdp.AggregateParams(metrics=[pdp.Metrics.COUNT, pdp.Metrics.SUM,
+                                          pdp.Metrics.PRIVACY_ID_COUNT],
+                                 max_partitions_contributed=2, max_contributions_per_partition=1,
+                                 min_value=0.0, max_value=10.0)
+    res, _ = run_engine(pid, pk, val, params, public=list(range(P)), n_partitions=P)
+    ref = oracle.bound_aggregate(pid, pk, val, res.last_bound_fields, SEED,
+                                 public_mask=oracle.bitmap(range(P), P))
+    got = {k: v.cpu().numpy() for k, v in res.last_partials.items() if v is not None}
+    assert np.array_equal(got["rows"], ref["rows"])
+    assert np.array_equal(got["count"], ref["count"])
+    assert np.allclose(got["sum"], ref["sum"], rtol=1e-9, atol=1e-9)
+
+
 def test_gpu_empty_and_single_record(built):
     params = pdp.AggregateParams(metrics=[pdp.Metrics.COUNT, pdp.Metrics.SUM],
                                  max_partitions_contributed=1, max_contributions_per_partition=1,
