@@ -34,6 +34,16 @@ __host__ __device__ constexpr size_t a16(size_t x) { return (x + 15) & ~(size_t)
 
 typedef int64_t i64x2 __attribute__((ext_vector_type(2)));
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+typedef uint64_t u64x2a8 __attribute__((ext_vector_type(2), aligned(8)));
+
+template <class Src, class = void>
+struct HasFetchPairs {
+    static constexpr bool value = false;
+};
+template <class Src>
+struct HasFetchPairs<Src, decltype((void)Src::kFetchPairs)> {
+    static constexpr bool value = Src::kFetchPairs;
+};
 
 // Sources without a pair view (kPairs false) take the one-record loop.
 template <class Src, class = void>
@@ -161,8 +171,17 @@ struct SrcAoS {
         d = digit(a[i]);
         return true;
     }
-    // 8-byte records: pairs by 16-byte loads (see SrcSoAKey::hist2)
+    // 8-byte records: pairs by 16-byte loads (see SrcSoAKey::hist2); the
+    // scatter's fetch2 needs only 8-byte alignment (any tile start)
     static constexpr bool kPairs = sizeof(R) == 8;
+    static constexpr bool kFetchPairs = sizeof(R) == 8;
+    __device__ __forceinline__ void fetch2(int64_t i, R &x0, R &x1) const {
+        if constexpr (sizeof(R) == 8) {
+            const u64x2a8 w = *reinterpret_cast<const u64x2a8 *>(a + i);
+            x0 = R{w.x};
+            x1 = R{w.y};
+        }
+    }
     __device__ __forceinline__ bool pairs_ok() const { return ((uintptr_t)a & 15) == 0; }
     __device__ __forceinline__ void hist2(int64_t i, uint32_t (&d)[2], bool (&ok)[2]) const {
         if constexpr (sizeof(R) == 8) {
@@ -653,6 +672,7 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
                                                           uint32_t C = 1) {
     constexpr int SUB = kScatThreads * IPT;
     constexpr bool kSD = !Src::kDigitFromRec;
+    constexpr bool kP = HasFetchPairs<Src>::value && IPT % 2 == 0;
     using W = Words<Rec>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     W *stage = reinterpret_cast<W *>(smem);  // [SUB + 1]: slot SUB takes dropped records
@@ -669,6 +689,11 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
     // segments at the same time and their runs meet in that XCD's L2
     const uint32_t nt = *ntiles;
     const int tid = threadIdx.x;
+    // sub-tile position of this thread's element j
+    auto elem = [tid](int j) -> uint32_t {
+        return kP ? (uint32_t)((j >> 1) * 2 * kScatThreads + 2 * tid + (j & 1))
+                  : (uint32_t)(j * kScatThreads + tid);
+    };
     __shared__ uint32_t sh_next;
     const uint32_t xq_id = blockIdx.x & 7u;
     const uint32_t xq_len = xq.q ? xq.n[xq_id] : 0u;
@@ -707,13 +732,30 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
     // Every LDS step below is likewise branch-free: a predicated LDS access
     // whose result is used becomes a branch with an lgkmcnt(0) wait inside,
     // which serialises the IPT accesses of a thread.
+    // Pair sources: element j of a thread is sub-tile position
+    // (j / 2) * 2T + 2 tid + j % 2, so elements 2m, 2m + 1 load as one
+    // 16-byte load (clamped to the last two records; a one-record sub-tile
+    // loads singly)
     typename Src::Raw raw[IPT];
-    {
-        const uint32_t lim = (uint32_t)min<int64_t>(SUB, td.end - td.begin);
+    auto load_sub = [&](int64_t b0, uint32_t lim) {
+        if constexpr (kP) {
+            if (lim >= 2) {
 #pragma unroll
-        for (int j = 0; j < IPT; ++j)
-            raw[j] = src.fetch(td.begin + min((uint32_t)(j * kScatThreads + tid), lim - 1));
-    }
+                for (int m = 0; m < IPT / 2; ++m) {
+                    const uint32_t o = m * 2 * kScatThreads + 2 * tid;
+                    const uint32_t a = min(o, lim - 2);
+                    typename Src::Raw x0, x1;
+                    src.fetch2(b0 + a, x0, x1);
+                    raw[2 * m] = a == o ? x0 : x1;
+                    raw[2 * m + 1] = x1;
+                }
+                return;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < IPT; ++j) raw[j] = src.fetch(b0 + min(elem(j), lim - 1));
+    };
+    load_sub(td.begin, (uint32_t)min<int64_t>(SUB, td.end - td.begin));
     __syncthreads();
     for (int64_t sb = td.begin; sb < td.end; sb += SUB) {
         const uint32_t lim = (uint32_t)min<int64_t>(SUB, td.end - sb);  // uniform
@@ -727,7 +769,7 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
             bool okv[IPT];
 #pragma unroll
             for (int j = 0; j < IPT; ++j) {
-                const uint32_t o = j * kScatThreads + tid;
+                const uint32_t o = elem(j);
                 uint32_t d = 0;
                 okv[j] = o < lim && src.decode(raw[j], sb + o, rec[j], d);
                 dg[j] = okv[j] ? d : 0u;
@@ -742,7 +784,7 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
             // serialisation
 #pragma unroll
             for (int j = 0; j < IPT; ++j) {
-                const uint32_t o = j * kScatThreads + tid;
+                const uint32_t o = elem(j);
                 uint32_t d = 0;
                 const bool ok = o < lim && src.decode(raw[j], sb + o, rec[j], d);
                 const uint32_t rk = wave_agg_rank(cnt, ok ? d : 0u, ok, bits);
@@ -766,11 +808,7 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
         __syncthreads();
         const int64_t nb = sb + SUB;
         const uint32_t nlim = (uint32_t)max<int64_t>(0, min<int64_t>(SUB, td.end - nb));
-        if (nlim > 0) {
-#pragma unroll
-            for (int j = 0; j < IPT; ++j)
-                raw[j] = src.fetch(nb + min((uint32_t)(j * kScatThreads + tid), nlim - 1));
-        }
+        if (nlim > 0) load_sub(nb, nlim);
         // write-out in batches of WB staged records per thread, branch-free:
         // slots past the end repeat the last staged record, whose store they
         // duplicate (same value, same address)

@@ -15,6 +15,10 @@ timeout -k 10 400 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.er
 python -c "import json; d=json.load(open('gpurun_out/bench.json')); print('c2 ms', round(d['ms_per_step'],2), 'frac', round(d['roofline']['frac'],4), 'cpu', d.get('cpu_baseline',{}).get('value'))"
 timeout -k 10 400 python bench.py --workload config4 --steps 4 --warmup 1 --no-cpu-baseline > gpurun_out/bench_c4.json 2> gpurun_out/bench_c4.err || { echo c4 failed; tail -20 gpurun_out/bench_c4.err; exit 1; }
 python -c "import json; d=json.load(open('gpurun_out/bench_c4.json')); print('c4 ms', round(d['ms_per_step'],2))"
+timeout -k 10 400 python bench.py --workload config4 --public --steps 4 --warmup 1 --no-cpu-baseline > gpurun_out/bench_c4p.json 2> gpurun_out/bench_c4p.err || { echo c4p failed; tail -20 gpurun_out/bench_c4p.err; exit 1; }
+python -c "import json; d=json.load(open('gpurun_out/bench_c4p.json')); print('c4 public ms', round(d['ms_per_step'],2))"
+timeout -k 10 400 python bench.py --workload config5 --steps 3 --warmup 1 > gpurun_out/bench_c5.json 2> gpurun_out/bench_c5.err || { echo c5 failed; tail -20 gpurun_out/bench_c5.err; exit 1; }
+python -c "import json; d=json.load(open('gpurun_out/bench_c5.json')); print('c5 ms', round(d['ms_per_step'],2))"
 cd /tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof/kt -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $R/gpurun_out/prof/kt_bench.json 2> $R/gpurun_out/prof/kt.err || { echo kt failed; tail -20 $R/gpurun_out/prof/kt.err; exit 1; }
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/prof/pmc_fetch -o run -- python3 $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline > /dev/null 2> $R/gpurun_out/prof/pmc_fetch.err || { echo fetch failed; tail -20 $R/gpurun_out/prof/pmc_fetch.err; exit 1; }
