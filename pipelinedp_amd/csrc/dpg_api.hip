@@ -83,9 +83,15 @@ namespace {
 
 // Debug watchdog (env DPG_WATCHDOG_S=<seconds>): instead of blocking, poll
 // the stream; on timeout print each workgroup's last phase and abort.
+// Debug builds only (-DDPG_WATCHDOG or the timing build): the product
+// kernels do not record their phases.
 int watchdog_seconds() {
+#if defined(DPG_WATCHDOG) || defined(DPG_PHASE_TIMING)
     const char *e = std::getenv("DPG_WATCHDOG_S");
     return e ? std::atoi(e) : 0;
+#else
+    return 0;
+#endif
 }
 
 uint32_t *watchdog_buffer(size_t n) {

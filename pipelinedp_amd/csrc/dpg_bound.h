@@ -69,10 +69,15 @@ struct PhaseTimer {
 #else
 struct PhaseTimer {};
 #endif
+// The watchdog store is compiled into the debug builds only (-DDPG_WATCHDOG
+// or the timing build): in the product kernels its pointer and branch cost
+// scalar registers the bounding kernel spills.
 __device__ __forceinline__ void mark(const BoundParams &bp, uint32_t phase, PhaseTimer &tm) {
+#if defined(DPG_WATCHDOG) || defined(DPG_PHASE_TIMING)
     if (bp.progress && threadIdx.x == 0)
         __hip_atomic_store(&bp.progress[blockIdx.x], phase, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
+#endif
 #ifdef DPG_PHASE_TIMING
     if (bp.phase_cyc) {
         const uint64_t now = __builtin_amdgcn_s_memtime();

@@ -972,6 +972,19 @@ __global__ __launch_bounds__(64, kWCap <= 384 ? 3 : 2) void k_bound_waves(const 
     bp.pid_min = vreg(bp.pid_min);
     bp.rec_base = vreg(bp.rec_base);
     bp.hash.mask = vreg(bp.hash.mask);
+    // bounds and record-format fields only meet vector operands
+    bp.mpc = vreg(bp.mpc);
+    bp.mcpp = vreg(bp.mcpp);
+    bp.L = vreg(bp.L);
+    bp.fmt.ib = vreg(bp.fmt.ib);
+    bp.fmt.pkbits = vreg(bp.fmt.pkbits);
+    bp.fmt.kbits = vreg(bp.fmt.kbits);
+    bp.fmt.b1 = vreg(bp.fmt.b1);
+    // pointers used by one phase each (or only on errors)
+    bp.value = vreg(bp.value);
+    bp.err = vreg(bp.err);
+    bp.heavy_fb = vreg(bp.heavy_fb);
+    bp.heavy_nfb = vreg(bp.heavy_nfb);
     bp.hash.i1 = vreg(bp.hash.i1);
     bp.hash.i2 = vreg(bp.hash.i2);
     const uint32_t nch = __builtin_amdgcn_readfirstlane(*n_chunks);
