@@ -273,9 +273,11 @@ class UtilityAnalysis:
         return torch.nonzero(has).flatten()
 
     # ------------------------------------------------ cross-partition combine
-    def _report(self, c: int, v: np.ndarray) -> metrics.UtilityReport:
+    def _report(self, c: int, v: list) -> metrics.UtilityReport:
         """UtilityReport of configuration c from its summed fields v (the
-        field layout of dpg_utility_analysis' report output)."""
+        field layout of dpg_utility_analysis' report output, as a list of
+        Python floats: per-element numpy scalar access dominated the report
+        assembly of a 64-configuration sweep)."""
         public = self.public is not None
         if public:
             info = metrics.PartitionsInfo(public_partitions=True,
@@ -289,39 +291,36 @@ class UtilityAnalysis:
             info = metrics.PartitionsInfo(public_partitions=False,
                                           num_dataset_partitions=int(round(v[0])),
                                           strategy=self.strategies[-1],
-                                          kept_partitions=metrics.MeanVariance(float(v[2]),
-                                                                               float(v[3])))
+                                          kept_partitions=metrics.MeanVariance(v[2], v[3]))
         report = metrics.UtilityReport(configuration_index=c, partitions_info=info)
         if not self.metrics:
             return report
-        total_w = float(v[1])
+        total_w = v[1]
         wscale = 0.0 if total_w == 0 else 1.0 / total_w
         errs = []
         cf = self.configs[c]
-        user_metrics = list(self.options.aggregate_params.metrics)
-        for mi, m in enumerate(self.metrics):
-            b = 4 + 24 * mi
-            tot, dd = float(v[b]), v[b + 1:b + 4]
-            dscale = 1.0 if tot == 0 else 1.0 / tot
-            a, r = v[b + 4:b + 14] * wscale, v[b + 14:b + 24] * wscale
+        noise_kind = cf.params.noise_kind
 
-            def verr(x):
-                return metrics.ValueErrors(
-                    bounding_errors=metrics.ContributionBoundingErrors(
-                        l0=metrics.MeanVariance(mean=float(x[0]), var=float(x[1])),
-                        linf_min=float(x[2]), linf_max=float(x[3])),
-                    mean=float(x[4]), variance=float(x[5]), rmse=float(x[6]), l1=float(x[7]),
-                    rmse_with_dropped_partitions=float(x[8]),
-                    l1_with_dropped_partitions=float(x[9]))
-            # the reference labels metric_errors by zipping them with the
-            # user's metric order (cross_partition_combiners.py:208-212)
+        def verr(x):
+            return metrics.ValueErrors(
+                bounding_errors=metrics.ContributionBoundingErrors(
+                    l0=metrics.MeanVariance(mean=x[0] * wscale, var=x[1] * wscale),
+                    linf_min=x[2] * wscale, linf_max=x[3] * wscale),
+                mean=x[4] * wscale, variance=x[5] * wscale, rmse=x[6] * wscale,
+                l1=x[7] * wscale, rmse_with_dropped_partitions=x[8] * wscale,
+                l1_with_dropped_partitions=x[9] * wscale)
+        # the reference labels metric_errors by zipping them with the user's
+        # metric order (cross_partition_combiners.py:208-212)
+        for mi, (m, um, std) in enumerate(zip(self.metrics, self._user_metrics, cf.std_list)):
+            b = 4 + 24 * mi
+            tot = v[b]
+            dscale = 1.0 if tot == 0 else 1.0 / tot
             errs.append(metrics.MetricUtility(
-                metric=user_metrics[mi], noise_std=cf.noise_std[m],
-                noise_kind=cf.params.noise_kind,
-                ratio_data_dropped=metrics.DataDropInfo(l0=float(dd[0] * dscale),
-                                                        linf=float(dd[1] * dscale),
-                                                        partition_selection=float(dd[2] * dscale)),
-                absolute_error=verr(a), relative_error=verr(r)))
+                metric=um, noise_std=std, noise_kind=noise_kind,
+                ratio_data_dropped=metrics.DataDropInfo(l0=v[b + 1] * dscale,
+                                                        linf=v[b + 2] * dscale,
+                                                        partition_selection=v[b + 3] * dscale),
+                absolute_error=verr(v[b + 4:b + 14]), relative_error=verr(v[b + 14:b + 24])))
         report.metric_errors = errs
         return report
 
@@ -331,14 +330,18 @@ class UtilityAnalysis:
         report fields per (size bucket, configuration)."""
         self.run()
         byb = self.rep.permute(0, 2, 1).cpu().numpy()        # [bucket, C, F]
-        present = byb[:, 0, 0] > 0
-        tot = byb.sum(axis=0)                                 # [C, F]
+        present = np.nonzero(byb[:, 0, 0] > 0)[0].tolist()
+        tot = byb.sum(axis=0).tolist()                        # [C][F]
+        rows = {bi: byb[bi].tolist() for bi in present}       # bucket -> [C][F]
+        self._user_metrics = list(self.options.aggregate_params.metrics)
+        for cf in self.configs:
+            cf.std_list = [cf.noise_std[m] for m in self.metrics]
+        bins = [(bi, BUCKET_BOUNDS[bi], _get_upper_bound(BUCKET_BOUNDS[bi])) for bi in present]
         out = []
         for c in range(len(self.configs)):
             rep = self._report(c, tot[c])
-            hist = [metrics.UtilityReportBin(BUCKET_BOUNDS[bi], _get_upper_bound(BUCKET_BOUNDS[bi]),
-                                             self._report(c, byb[bi, c]))
-                    for bi in np.nonzero(present)[0]]
+            hist = [metrics.UtilityReportBin(lo, hi, self._report(c, rows[bi][c]))
+                    for bi, lo, hi in bins]
             rep.utility_report_histogram = hist if hist else None
             out.append(rep)
         return out
