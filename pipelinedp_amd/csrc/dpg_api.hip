@@ -341,7 +341,9 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     int st = DPG_OK;
     using CL = ChunkLayout<KeyT, Item>;
     using WL = WaveLayout<KeyT, Item>;
-    const uint32_t capM = std::min<uint32_t>(ctx->bucket_cap, (uint32_t)kBCap);
+    uint32_t capM = std::min<uint32_t>(ctx->bucket_cap, (uint32_t)kBCap);
+    if (const char *e = std::getenv("DPG_DEBUG_CAP"))  // debug: medium-chunk experiments
+        capM = std::max<uint32_t>(1, std::min<uint32_t>(capM, (uint32_t)std::atoi(e)));
     // small chunks need <= 7 pid hash bits below a bucket (kWCq = 128 slots)
     auto cap_small = [&](uint32_t plb) {
         return plb <= 7 ? std::min<uint32_t>(capM, (uint32_t)kWCap) : 0u;
