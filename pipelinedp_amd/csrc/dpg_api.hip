@@ -287,7 +287,10 @@ int run_level(dpg_ctx *ctx, hipStream_t s, const Src &src, uint32_t S, const int
 // record; later levels recompute it
 template <class R>
 struct Ipt {
-    static constexpr int L1 = sizeof(R) == 8 ? 12 : 8;
+#ifndef DPG_IPT_L1
+#define DPG_IPT_L1 12
+#endif
+    static constexpr int L1 = sizeof(R) == 8 ? DPG_IPT_L1 : 8;
     static constexpr int LN = sizeof(R) == 8 ? 16 : 10;
     // the refine level has few digits (wave-aggregated ranking, which holds
     // more registers per record: at LN records per thread it spilled)
