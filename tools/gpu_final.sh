@@ -23,6 +23,8 @@ cd /tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof/kt -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $R/gpurun_out/prof/kt_bench.json 2> $R/gpurun_out/prof/kt.err || { echo kt failed; tail -20 $R/gpurun_out/prof/kt.err; exit 1; }
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/prof/pmc_fetch -o run -- python3 $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline > /dev/null 2> $R/gpurun_out/prof/pmc_fetch.err || { echo fetch failed; tail -20 $R/gpurun_out/prof/pmc_fetch.err; exit 1; }
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/prof/pmc_write -o run -- python3 $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline > /dev/null 2> $R/gpurun_out/prof/pmc_write.err || { echo write failed; tail -20 $R/gpurun_out/prof/pmc_write.err; exit 1; }
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/prof/c4_fetch -o run -- python3 $R/bench.py --workload config4 --steps 1 --warmup 1 --no-cpu-baseline > /dev/null 2> $R/gpurun_out/prof/c4_fetch.err || { echo c4 fetch failed; tail -20 $R/gpurun_out/prof/c4_fetch.err; exit 1; }
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/prof/c4_write -o run -- python3 $R/bench.py --workload config4 --steps 1 --warmup 1 --no-cpu-baseline > /dev/null 2> $R/gpurun_out/prof/c4_write.err || { echo c4 write failed; tail -20 $R/gpurun_out/prof/c4_write.err; exit 1; }
 timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/prof/cal_fetch -o run -- $R/tools/calib_fetch > $R/gpurun_out/prof/cal.json 2> $R/gpurun_out/prof/cal_fetch.err || { echo cal fetch failed; tail -5 $R/gpurun_out/prof/cal_fetch.err; exit 1; }
 timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/prof/cal_write -o run -- $R/tools/calib_fetch > /dev/null 2> $R/gpurun_out/prof/cal_write.err || { echo cal write failed; tail -5 $R/gpurun_out/prof/cal_write.err; exit 1; }
 cd $R
