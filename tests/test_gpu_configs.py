@@ -3,8 +3,9 @@ finishes in seconds): the config-2 generator at 1e7 records, and the config-4
 shape (Pareto(1.2) records per privacy id, mpc = 50, mcpp = 4, P = 1e8,
 MEAN+VARIANCE with Gaussian noise) with public and with private partitions.
 The config-4 data holds privacy ids with tens of thousands of records, so
-their buckets take the global-memory kernel (k_bound_big) with 32-byte
-MEAN/VARIANCE items."""
+their buckets take the heavy-id filter and the global-memory kernel
+(k_bound_big), with 24-byte MEAN/VARIANCE items (ItemV: no SUM requested) and
+12-byte records (P = 1e8 needs a 70-bit record key)."""
 import numpy as np
 import pytest
 import torch
@@ -114,9 +115,10 @@ def _c4_params():
 
 
 def test_config4_public_partitions_match_oracle(built, config4_data):
-    """public_partitions = range(1e8): non-public drop + empty partitions,
-    MEAN/VARIANCE moments through every bounding kernel (Item32), noise-free
-    outputs equal the oracle's for all 1e8 partitions."""
+    """public_partitions = range(1e8): empty partitions kept (the set covers
+    every id, so level 1 drops nothing), MEAN/VARIANCE moments through every
+    bounding kernel (ItemV), noise-free outputs equal the oracle's for all
+    1e8 partitions."""
     pid, pk, val = config4_data
     res, out, got = _run(pid, pk, val, _c4_params(), P4, public=range(P4))
     mask = np.full((P4 + 7) // 8, 0xFF, np.uint8)
