@@ -6,7 +6,7 @@ from typing import List, Optional
 from pipelinedp_amd import aggregate_params as agg
 
 
-@dataclass
+@dataclass(slots=True)
 class SumMetrics:
     """Per-partition error terms of one DP metric (COUNT, PRIVACY_ID_COUNT
     or SUM): E(bounded value) = sum + clipping_to_min_error +
@@ -21,26 +21,26 @@ class SumMetrics:
     noise_kind: agg.NoiseKind
 
 
-@dataclass
+@dataclass(slots=True)
 class RawStatistics:
     privacy_id_count: int
     count: int
 
 
-@dataclass
+@dataclass(slots=True)
 class PerPartitionMetrics:
     partition_selection_probability_to_keep: float
     raw_statistics: RawStatistics
     metric_errors: Optional[List[SumMetrics]] = None
 
 
-@dataclass
+@dataclass(slots=True)
 class MeanVariance:
     mean: float
     var: float
 
 
-@dataclass
+@dataclass(slots=True)
 class ContributionBoundingErrors:
     l0: MeanVariance
     linf_min: float
@@ -52,7 +52,7 @@ class ContributionBoundingErrors:
             linf_min=self.linf_min / value, linf_max=self.linf_max / value)
 
 
-@dataclass
+@dataclass(slots=True)
 class ValueErrors:
     """Errors of (dp_value - actual_value) averaged across partitions; the
     *_with_dropped_partitions variants count dropped partitions as error."""
@@ -76,14 +76,14 @@ class ValueErrors:
                            l1_with_dropped_partitions=self.l1_with_dropped_partitions / value)
 
 
-@dataclass
+@dataclass(slots=True)
 class DataDropInfo:
     l0: float
     linf: float
     partition_selection: float
 
 
-@dataclass
+@dataclass(slots=True)
 class MetricUtility:
     metric: agg.Metric
     noise_std: float
@@ -93,7 +93,7 @@ class MetricUtility:
     relative_error: ValueErrors
 
 
-@dataclass
+@dataclass(slots=True)
 class PartitionsInfo:
     public_partitions: bool
     num_dataset_partitions: int
@@ -103,7 +103,7 @@ class PartitionsInfo:
     kept_partitions: Optional[MeanVariance] = None
 
 
-@dataclass
+@dataclass(slots=True)
 class UtilityReport:
     configuration_index: int
     partitions_info: PartitionsInfo
@@ -111,7 +111,7 @@ class UtilityReport:
     utility_report_histogram: Optional[List["UtilityReportBin"]] = None
 
 
-@dataclass
+@dataclass(slots=True)
 class UtilityReportBin:
     """Report of the partitions whose size lies in [partition_size_from,
     partition_size_to)."""
