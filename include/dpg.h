@@ -352,6 +352,27 @@ int dpg_dataset_histograms(dpg_ctx *ctx, const dpg_pair_entry *pairs, int64_t n_
 /* Timing/profiling aid: per-stage device time (ms) of the last
  * dpg_bound_aggregate call, measured with HIP events on its stream.
  * names: "hist1","scatter1","hist2","scatter2","process","reduce", ... */
+/* ---- multi-GPU: an RCCL communicator for the partial merge ----
+ * One process per GPU, records sharded by privacy id (bounding is then
+ * shard-local).  Rank 0 calls dpg_comm_unique_id; the
+ * DPG_COMM_ID_BYTES bytes reach every rank by the host's own means (MPI,
+ * TCP, a shared file); each rank then attaches a communicator to its
+ * context.  RCCL is loaded on first use (dlopen of librccl), so libdpg.so
+ * has no link-time dependency on it and shares the copy a host such as
+ * PyTorch has already loaded.  Replaces the reference's shuffle of
+ * (partition key, accumulator) pairs between workers
+ * (pipeline_backend.py:712-823, combine_accumulators_per_key on Beam/Spark). */
+#define DPG_COMM_ID_BYTES 128
+int dpg_comm_unique_id(uint8_t *id);
+int dpg_ctx_create_comm(dpg_ctx *ctx, const uint8_t *id, int rank, int nranks);
+/* Sums the dense partials of every rank (ONE ncclReduceScatter of all
+ * non-null arrays packed as float64 -- exact below 2^53) and writes this
+ * rank's slice [lo, lo + n), lo = rank * S, S = ceil(P / nranks), into
+ * `slice` (its arrays hold >= S entries; the same arrays non-null as in
+ * `full`; slice->n_partitions is set to n).  Stream-ordered on `stream`. */
+int dpg_reduce_scatter_partials(dpg_ctx *ctx, const dpg_partials *full, dpg_partials *slice,
+                                int64_t *lo, int64_t *n, void *stream);
+
 int dpg_last_stage_times(dpg_ctx *ctx, char *names, size_t names_len,
                          double *ms, int32_t max_stages, int32_t *n_stages);
 

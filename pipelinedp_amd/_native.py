@@ -18,7 +18,10 @@ EXPORTED = ("dpg_ctx_create", "dpg_ctx_destroy", "dpg_last_error", "dpg_set_seed
             "dpg_set_tuning",
             "dpg_bound_aggregate", "dpg_select_and_noise", "dpg_compact_kept",
             "dpg_last_stage_times", "dpg_stream_seed", "dpg_preaggregate",
-            "dpg_utility_analysis", "dpg_dataset_histograms")
+            "dpg_utility_analysis", "dpg_dataset_histograms",
+            "dpg_comm_unique_id", "dpg_ctx_create_comm", "dpg_reduce_scatter_partials")
+
+COMM_ID_BYTES = 128  # DPG_COMM_ID_BYTES
 
 HIST_INT_BINS = 16300  # DPG_HIST_INT_BINS
 HIST_SUM_BINS = 10000  # DPG_HIST_SUM_BINS
@@ -171,6 +174,15 @@ def load():
                                              ctypes.POINTER(ctypes.c_double), i32,
                                              ctypes.POINTER(ctypes.c_int32)]
         lib.dpg_last_stage_times.restype = ctypes.c_int
+        lib.dpg_comm_unique_id.argtypes = [ctypes.c_char_p]
+        lib.dpg_comm_unique_id.restype = ctypes.c_int
+        lib.dpg_ctx_create_comm.argtypes = [vp, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]
+        lib.dpg_ctx_create_comm.restype = ctypes.c_int
+        lib.dpg_reduce_scatter_partials.argtypes = [vp, ctypes.POINTER(Partials),
+                                                    ctypes.POINTER(Partials),
+                                                    ctypes.POINTER(ctypes.c_int64),
+                                                    ctypes.POINTER(ctypes.c_int64), vp]
+        lib.dpg_reduce_scatter_partials.restype = ctypes.c_int
         _lib = lib
         return lib
 
@@ -225,6 +237,26 @@ class Context:
         st = self.lib.dpg_bound_aggregate(self.handle, pid_ptr, pk_ptr, value_ptr, n,
                                           ctypes.byref(bound), ctypes.byref(partials), stream)
         self.check(st, "dpg_bound_aggregate")
+
+    def comm_unique_id(self) -> bytes:
+        """RCCL unique id (rank 0), DPG_COMM_ID_BYTES opaque bytes."""
+        buf = ctypes.create_string_buffer(COMM_ID_BYTES)
+        self.check(self.lib.dpg_comm_unique_id(buf), "dpg_comm_unique_id")
+        return buf.raw
+
+    def create_comm(self, uid: bytes, rank: int, nranks: int):
+        self.check(self.lib.dpg_ctx_create_comm(self.handle, uid, rank, nranks),
+                   "dpg_ctx_create_comm")
+
+    def reduce_scatter_partials(self, full: Partials, slice_: Partials, stream):
+        """Sums every rank's partials; this rank's slice (lo, n) lands in
+        slice_ (see dpg.h)."""
+        lo, n = ctypes.c_int64(0), ctypes.c_int64(0)
+        st = self.lib.dpg_reduce_scatter_partials(self.handle, ctypes.byref(full),
+                                                  ctypes.byref(slice_), ctypes.byref(lo),
+                                                  ctypes.byref(n), stream)
+        self.check(st, "dpg_reduce_scatter_partials")
+        return lo.value, n.value
 
     def select_and_noise(self, partials: Partials, sel: SelectParams, noise: NoiseParams,
                          keep_ptr, out_ptr, stream):

@@ -10,7 +10,9 @@
 //      chunks), refine level for oversize buckets -> k_bound_chunks
 //      (+ k_bound_big for single buckets still over the chunk capacity)
 //   -> one partition-key-range level over the kept pairs -> k_reduce_items
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>  // types and enums only: the functions are resolved by dlsym
 
 #include <algorithm>
 #include <chrono>
@@ -77,6 +79,8 @@ struct dpg_ctx {
     hipStream_t last_stream = nullptr;
     uint32_t bucket_target = 0;  // 0: kBucketTarget
     uint32_t bucket_cap = kBCap;
+    void *comm = nullptr;        // ncclComm_t (dpg_ctx_create_comm)
+    int rank = 0, nranks = 1;
 };
 
 namespace {
@@ -858,6 +862,89 @@ int aggregate_impl(dpg_ctx *ctx, const int64_t *pid, const int64_t *pk, const do
 
 }  // namespace
 
+namespace {
+
+// ---------------------------------------------------------------- RCCL
+// Resolved at first use from the librccl already in the process (a host
+// such as PyTorch loads its own) or from the ROCm install; libdpg.so does
+// not link it.
+struct Rccl {
+    bool tried = false, ok = false;
+    ncclResult_t (*get_unique_id)(ncclUniqueId *) = nullptr;
+    ncclResult_t (*comm_init_rank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*reduce_scatter)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t,
+                                   ncclComm_t, hipStream_t) = nullptr;
+    const char *(*error_string)(ncclResult_t) = nullptr;
+};
+
+Rccl &rccl() {
+    static Rccl r;
+    if (r.tried) return r;
+    r.tried = true;
+    void *h = nullptr;
+    for (const char *name : {"librccl.so.1", "librccl.so"})
+        if (!h) h = dlopen(name, RTLD_NOW | RTLD_NOLOAD);
+    for (const char *name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
+        if (!h) h = dlopen(name, RTLD_NOW | RTLD_GLOBAL);
+    if (!h) return r;
+    r.get_unique_id = (decltype(r.get_unique_id))dlsym(h, "ncclGetUniqueId");
+    r.comm_init_rank = (decltype(r.comm_init_rank))dlsym(h, "ncclCommInitRank");
+    r.comm_destroy = (decltype(r.comm_destroy))dlsym(h, "ncclCommDestroy");
+    r.reduce_scatter = (decltype(r.reduce_scatter))dlsym(h, "ncclReduceScatter");
+    r.error_string = (decltype(r.error_string))dlsym(h, "ncclGetErrorString");
+    r.ok = r.get_unique_id && r.comm_init_rank && r.comm_destroy && r.reduce_scatter;
+    return r;
+}
+
+std::string rccl_msg(ncclResult_t e) {
+    const Rccl &r = rccl();
+    return r.error_string ? std::string(r.error_string(e)) : "RCCL error " + std::to_string((int)e);
+}
+
+// Partials to the reduce-scatter layout [rank][array][S] (float64, zero
+// padded past P) and back (integer arrays are exact in float64 below 2^53).
+struct PackArrays {
+    const void *a[5];
+    int is_int[5];
+    int n;
+};
+
+__global__ void k_pack_partials(PackArrays src, int64_t P, int64_t S, int nranks, double *pack) {
+    const int64_t total = S * nranks;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < total;
+         k += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = k / S, i = k - r * S;
+        for (int j = 0; j < src.n; ++j) {
+            double v = 0.0;
+            if (k < P)
+                v = src.is_int[j] ? (double)static_cast<const int64_t *>(src.a[j])[k]
+                                  : static_cast<const double *>(src.a[j])[k];
+            pack[(r * src.n + j) * S + i] = v;
+        }
+    }
+}
+
+struct UnpackArrays {
+    void *a[5];
+    int is_int[5];
+    int n;
+};
+
+__global__ void k_unpack_partials(const double *part, int64_t S, int64_t n_local,
+                                  UnpackArrays dst) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_local;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        for (int j = 0; j < dst.n; ++j) {
+            const double v = part[j * S + i];
+            if (dst.is_int[j]) static_cast<int64_t *>(dst.a[j])[i] = (int64_t)llrint(v);
+            else static_cast<double *>(dst.a[j])[i] = v;
+        }
+    }
+}
+
+}  // namespace
+
 extern "C" {
 
 dpg_ctx *dpg_ctx_create(int device, uint64_t seed) {
@@ -873,6 +960,7 @@ dpg_ctx *dpg_ctx_create(int device, uint64_t seed) {
 void dpg_ctx_destroy(dpg_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
+    if (c->comm && rccl().ok) (void)rccl().comm_destroy(static_cast<ncclComm_t>(c->comm));
     for (auto &kv : c->bufs)
         if (kv.second.p) (void)hipFree(kv.second.p);
     for (auto e : c->events) (void)hipEventDestroy(e);
@@ -1311,6 +1399,85 @@ int dpg_last_stage_times(dpg_ctx *ctx, char *names, size_t names_len, double *ms
         joined += ctx->stage_names[i];
     }
     if (names && names_len) std::snprintf(names, names_len, "%s", joined.c_str());
+    return DPG_OK;
+}
+
+int dpg_comm_unique_id(uint8_t *id) {
+    if (!id) return DPG_ERR_INVALID_ARG;
+    Rccl &r = rccl();
+    if (!r.ok) return DPG_ERR_UNSUPPORTED;
+    ncclUniqueId u;
+    if (r.get_unique_id(&u) != ncclSuccess) return DPG_ERR_HIP;
+    static_assert(sizeof(u) == DPG_COMM_ID_BYTES, "unique id size");
+    std::memcpy(id, &u, DPG_COMM_ID_BYTES);
+    return DPG_OK;
+}
+
+int dpg_ctx_create_comm(dpg_ctx *ctx, const uint8_t *id, int rank, int nranks) {
+    if (!ctx || !id || nranks < 1 || rank < 0 || rank >= nranks) return DPG_ERR_INVALID_ARG;
+    Rccl &r = rccl();
+    if (!r.ok) return fail(ctx, DPG_ERR_UNSUPPORTED, "librccl could not be loaded");
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, DPG_ERR_HIP, "hipSetDevice");
+    if (ctx->comm) {
+        (void)r.comm_destroy(static_cast<ncclComm_t>(ctx->comm));
+        ctx->comm = nullptr;
+    }
+    ncclUniqueId u;
+    std::memcpy(&u, id, DPG_COMM_ID_BYTES);
+    ncclComm_t c = nullptr;
+    const ncclResult_t e = r.comm_init_rank(&c, nranks, u, rank);
+    if (e != ncclSuccess) return fail(ctx, DPG_ERR_HIP, "ncclCommInitRank: " + rccl_msg(e));
+    ctx->comm = c;
+    ctx->rank = rank;
+    ctx->nranks = nranks;
+    return DPG_OK;
+}
+
+int dpg_reduce_scatter_partials(dpg_ctx *ctx, const dpg_partials *full, dpg_partials *slice,
+                                int64_t *lo, int64_t *n, void *stream) {
+    if (!ctx || !full || !slice || !lo || !n) return DPG_ERR_INVALID_ARG;
+    if (!ctx->comm) return fail(ctx, DPG_ERR_INVALID_ARG, "no communicator: dpg_ctx_create_comm");
+    const int64_t P = full->n_partitions;
+    if (P <= 0) return fail(ctx, DPG_ERR_INVALID_ARG, "n_partitions must be positive");
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, DPG_ERR_HIP, "hipSetDevice");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    int st = DPG_OK;
+    const int R = ctx->nranks;
+    const int64_t S = (P + R - 1) / R;
+    PackArrays pa{};
+    UnpackArrays ua{};
+    const void *src[5] = {full->rows, full->count, full->sum, full->nsum, full->nsq};
+    void *dst[5] = {slice->rows, slice->count, slice->sum, slice->nsum, slice->nsq};
+    for (int k = 0; k < 5; ++k) {
+        if (!src[k]) continue;
+        if (!dst[k]) return fail(ctx, DPG_ERR_INVALID_ARG, "slice lacks an array the partials have");
+        pa.a[pa.n] = src[k];
+        pa.is_int[pa.n] = k < 2;
+        ua.a[ua.n] = dst[k];
+        ua.is_int[ua.n] = k < 2;
+        ++pa.n;
+        ++ua.n;
+    }
+    if (pa.n == 0) return fail(ctx, DPG_ERR_INVALID_ARG, "no partial arrays");
+    WS(pack, double, "comm.pack", (size_t)R * pa.n * S);
+    WS(part, double, "comm.part", (size_t)pa.n * S);
+    const int64_t total = S * R;
+    const unsigned blocks = (unsigned)std::min<int64_t>((total + 255) / 256, (int64_t)ctx->n_cu * 16);
+    k_pack_partials<<<blocks, 256, 0, s>>>(pa, P, S, R, pack);
+    LAUNCH_CHECK();
+    const ncclResult_t e = rccl().reduce_scatter(pack, part, (size_t)pa.n * S, ncclFloat64, ncclSum,
+                                                 static_cast<ncclComm_t>(ctx->comm), s);
+    if (e != ncclSuccess) return fail(ctx, DPG_ERR_HIP, "ncclReduceScatter: " + rccl_msg(e));
+    const int64_t l = std::min<int64_t>(P, (int64_t)ctx->rank * S);
+    const int64_t nl = std::min<int64_t>(P, l + S) - l;
+    if (nl > 0) {
+        const unsigned ub = (unsigned)std::min<int64_t>((nl + 255) / 256, (int64_t)ctx->n_cu * 16);
+        k_unpack_partials<<<ub, 256, 0, s>>>(part, S, nl, ua);
+        LAUNCH_CHECK();
+    }
+    *lo = l;
+    *n = nl;
+    slice->n_partitions = nl;
     return DPG_OK;
 }
 
