@@ -17,7 +17,14 @@ Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--records R]
        MEAN+VARIANCE, Gaussian, Pareto(1.2) records per privacy id, mpc = 50,
        mcpp = 4, 1e8 partitions; --public: public_partitions = range(1e8))
 --gpus N without a torch.distributed launcher re-launches itself as N ranks
-(torch.distributed.run, 127.0.0.1) before touching any GPU.
+(torch.distributed.run, 127.0.0.1) before touching any GPU.  Multi-rank
+options: --dist-backend nccl (RCCL, default; one GPU per rank) or gloo (host-
+staged collectives; ranks may share a GPU: rank r uses GPU r mod #GPUs, which
+is how a one-GPU box rehearses the N-rank path), --exchange auto |
+reduce_scatter | all_to_all (distributed.exchange_partials), --check-single
+(after timing, rank 0 re-runs the union of every rank's records as ONE rank
+with the release nonce of the N-rank run and reports whether the kept
+partition sets and the exact columns agree).
 """
 import argparse
 import hashlib
@@ -413,6 +420,11 @@ def main():
                     help="config4: cap of the Pareto weight of one privacy id")
     ap.add_argument("--cpu-records", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl")
+    ap.add_argument("--exchange", choices=["auto", "reduce_scatter", "all_to_all"],
+                    default="auto")
+    ap.add_argument("--check-single", action="store_true",
+                    help="multi-rank: compare the kept set with a one-rank run of all records")
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(_launch_ranks(args.gpus))
@@ -439,18 +451,25 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, args.partitions)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # device_count() does not initialise the GPU; gloo ranks may share one
+    ndev = max(1, torch.cuda.device_count())
+    gpu = local % ndev if args.dist_backend == "gloo" else local
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     group = None
     if world > 1:
-        torch.distributed.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            torch.distributed.init_process_group("nccl", device_id=dev)
+        else:
+            torch.distributed.init_process_group("gloo")
         group = torch.distributed.group.WORLD
     P = args.partitions
     pid_cdf = pareto_cdf(args.pids, 1.2, args.pid_cap, 4321, dev) if c4 else None
     pid, pk, val = generate(args.records, args.pids, P, rank, 1, dev, pid_cdf)
     del pid_cdf
     torch.cuda.synchronize()
-    backend = pdp.MI355XBackend(device=local, seed=0xD1FF5EED, process_group=group)
+    backend = pdp.MI355XBackend(device=gpu, seed=0xD1FF5EED, process_group=group,
+                                exchange=args.exchange)
     # the generator's privacy-id range and this rank's global record offset
     # are known metadata (like n_partitions): no device min/max pass
     cols = pdp.ColumnarData(pid=pid, pk=pk, value=val, n_partitions=P,
@@ -491,10 +510,15 @@ def main():
         torch.distributed.barrier()
     wall = time.perf_counter() - t0
     dev_ms = ev0.elapsed_time(ev1) / args.steps
-    t = torch.tensor([wall, dev_ms], dtype=torch.float64, device=dev)
+    per_rank = [[wall, dev_ms]]
     if group is not None:
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-    wall, dev_ms_max = float(t[0].item()), float(t[1].item())
+        cdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
+        mine = torch.tensor([wall, dev_ms], dtype=torch.float64, device=cdev)
+        got = [torch.zeros_like(mine) for _ in range(world)]
+        torch.distributed.all_gather(got, mine)
+        per_rank = [g.cpu().tolist() for g in got]
+    wall = max(r[0] for r in per_rank)
+    dev_ms_max = max(r[1] for r in per_rank)
     ms_per_step = wall / args.steps * 1e3
     total_records = args.records * world
     value = total_records / (wall / args.steps)
@@ -557,10 +581,72 @@ def main():
         line["roofline"]["traffic_by_kernel"] = tj.get("kernels")
     if cpu is not None:
         line["cpu_baseline"] = cpu
+    if group is not None:
+        # what the collectives actually saw, and every rank's own timing
+        line["distributed"] = {
+            "backend": torch.distributed.get_backend(group),
+            "world_size": torch.distributed.get_world_size(group),
+            "devices": ndev if args.dist_backend == "gloo" else world,
+            "exchange": res.last_exchange,
+            "rank_ms_per_step": [r[0] / args.steps * 1e3 for r in per_rank],
+            "rank_device_ms": [r[1] for r in per_rank]}
+        if args.check_single:
+            line["distributed"]["check_single"] = check_single(
+                args, cols, params, public, world, rank, dev, group)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if group is not None:
         torch.distributed.destroy_process_group()
+
+
+def check_single(args, cols, params, public, world, rank, dev, group):
+    """One N-rank release with a fixed nonce against ONE rank over the union
+    of every rank's records (rank 0 regenerates the other ranks' shards from
+    their seeds): the kept partition sets and the integer columns (count,
+    privacy id count) must be equal, sums equal to 1e-9."""
+    import pipelinedp_amd as pdp
+    nonce = 0x5EED0F2A11
+    ex = pdp.DataExtractors("pid", "pk", "value")
+    backend = pdp.MI355XBackend(device=dev.index, seed=0xD1FF5EED, process_group=group,
+                                exchange=args.exchange)
+    acc = pdp.NaiveBudgetAccountant(1.0, 1e-6)
+    res = pdp.DPEngine(acc, backend).aggregate(cols, params, ex, public_partitions=public)
+    acc.compute_budgets()
+    res.nonce = nonce
+    out = res.materialize(gather=True)
+    if rank != 0:
+        return None
+    ids_n = out.partition_ids.cpu().numpy()
+    vals_n = out.values.cpu().numpy()
+    P = args.partitions
+    pid_cdf = (pareto_cdf(args.pids, 1.2, args.pid_cap, 4321, dev)
+               if args.workload == "config4" else None)
+    parts = [generate(args.records, args.pids, P, r, 1, dev, pid_cdf) for r in range(world)]
+    pid = torch.cat([p[0] for p in parts])
+    pk = torch.cat([p[1] for p in parts])
+    val = torch.cat([p[2] for p in parts])
+    del parts
+    one = pdp.ColumnarData(pid=pid, pk=pk, value=val, n_partitions=P,
+                           privacy_id_range=(0, world * args.pids), record_id_offset=0)
+    acc1 = pdp.NaiveBudgetAccountant(1.0, 1e-6)
+    res1 = pdp.DPEngine(acc1, pdp.MI355XBackend(device=dev.index, seed=0xD1FF5EED)).aggregate(
+        one, params, ex, public_partitions=public)
+    acc1.compute_budgets()
+    res1.nonce = nonce
+    out1 = res1.materialize()
+    ids_1 = out1.partition_ids.cpu().numpy()
+    vals_1 = out1.values.cpu().numpy()
+    same_set = bool(np.array_equal(np.sort(ids_n), np.sort(ids_1)))
+    exact_cols = close_cols = False
+    if same_set:
+        o, o1 = np.argsort(ids_n), np.argsort(ids_1)
+        fields = list(res1.plan.fields)
+        ints = [j for j, f in enumerate(fields) if f in ("count", "privacy_id_count")]
+        exact_cols = bool(np.array_equal(vals_n[o][:, ints], vals_1[o1][:, ints]))
+        close_cols = bool(np.allclose(vals_n[o], vals_1[o1], rtol=1e-9, atol=1e-6))
+    return {"records": int(pid.numel()), "kept_n_rank": int(len(ids_n)),
+            "kept_one_rank": int(len(ids_1)), "same_kept_set": same_set,
+            "integer_columns_equal": exact_cols, "all_columns_close": close_cols}
 
 
 if __name__ == "__main__":

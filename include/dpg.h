@@ -339,7 +339,7 @@ int dpg_utility_analysis(dpg_ctx *ctx, const dpg_pair_entry *pairs,
 
 /* Dataset histograms over a pre-aggregate sorted by partition key (pairs,
  * partition_start as dpg_preaggregate writes them).  pre_aggregated = 0:
- * the pairs come from dpg_preaggregate, whose pad0 marks one pair per privacy
+ * the pairs come from dpg_preaggregate, whose `leader` marks one pair per privacy
  * id (the per-privacy-id histograms count those); 1: user-supplied
  * (count, sum, n_partitions, n_contributions) rows, L0 / L1 weighted by
  * 1 / n_partitions per exact value and rounded half to even
@@ -349,9 +349,6 @@ int dpg_dataset_histograms(dpg_ctx *ctx, const dpg_pair_entry *pairs, int64_t n_
                            const int64_t *partition_start, int64_t n_partitions,
                            int32_t pre_aggregated, const dpg_hist_out *out, void *stream);
 
-/* Timing/profiling aid: per-stage device time (ms) of the last
- * dpg_bound_aggregate call, measured with HIP events on its stream.
- * names: "hist1","scatter1","hist2","scatter2","process","reduce", ... */
 /* ---- multi-GPU: an RCCL communicator for the partial merge ----
  * One process per GPU, records sharded by privacy id (bounding is then
  * shard-local).  Rank 0 calls dpg_comm_unique_id; the
@@ -373,6 +370,14 @@ int dpg_ctx_create_comm(dpg_ctx *ctx, const uint8_t *id, int rank, int nranks);
 int dpg_reduce_scatter_partials(dpg_ctx *ctx, const dpg_partials *full, dpg_partials *slice,
                                 int64_t *lo, int64_t *n, void *stream);
 
+/* Timing/profiling aid: per-stage device time (ms) of the last
+ * dpg_bound_aggregate / dpg_preaggregate / dpg_dataset_histograms call,
+ * measured with HIP events on its stream (waits for the last event).
+ * names (comma separated, <= names_len bytes): e.g. "begin",
+ * "partition1:hist", "partition1:scatter", "partition2:hist",
+ * "partition2:scatter", "chunks", "bound.kernel=sort" (zero-length marker
+ * of the small-chunk kernel that ran), "bound", "bound.medium", "bound.tail",
+ * "items:hist", "items:scatter", "reduce". */
 int dpg_last_stage_times(dpg_ctx *ctx, char *names, size_t names_len,
                          double *ms, int32_t max_stages, int32_t *n_stages);
 

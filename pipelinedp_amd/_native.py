@@ -298,10 +298,10 @@ class Context:
         self.check(st, "dpg_dataset_histograms")
 
     def stage_times(self):
-        names = ctypes.create_string_buffer(1024)
-        ms = (ctypes.c_double * 32)()
+        names = ctypes.create_string_buffer(4096)
+        ms = (ctypes.c_double * 64)()
         ns = ctypes.c_int32(0)
-        self.check(self.lib.dpg_last_stage_times(self.handle, names, 1024, ms, 32,
+        self.check(self.lib.dpg_last_stage_times(self.handle, names, 4096, ms, 64,
                                                  ctypes.byref(ns)), "stage_times")
         keys = names.value.decode().split(",") if ns.value else []
         return dict(zip(keys, [ms[i] for i in range(ns.value)]))

@@ -105,6 +105,8 @@ def _sample_bound(prob: float) -> int:
 
 def _keep_by_hash(key, bound: int) -> bool:
     """sampling_utils.ValueSampler.keep (sampling_utils.py:32-51)."""
+    if isinstance(key, np.generic):  # hash what the reference's row key would print
+        key = key.item()
     h = int(hashlib.sha1(repr(key).encode()).hexdigest()[:16], 16)
     return h < bound
 

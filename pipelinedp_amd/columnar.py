@@ -288,6 +288,12 @@ def encode(col, extractors, device: torch.device, need_values: bool,
 
 
 def decode_keys(ids: np.ndarray, key_table) -> list:
+    """Dense ids -> the user's keys, as Python objects: a numpy key table
+    (integer tensor / array columns) yields Python scalars, so a key prints
+    and hashes as the reference's row keys do (e.g. repr 5, not
+    np.int64(5), which the utility analysis' partition sampler hashes)."""
     if key_table is None:
         return ids.tolist()
+    if isinstance(key_table, np.ndarray):
+        return key_table[ids].tolist()
     return [key_table[i] for i in ids.tolist()]

@@ -31,6 +31,7 @@
 #include "dpg_hist.h"
 #include "dpg_partition.h"
 #include "dpg_select.h"
+#include "dpg_sortb.h"
 #include "dpg_utility.h"
 #include "dpg_wave.h"
 
@@ -81,6 +82,10 @@ struct dpg_ctx {
     uint32_t bucket_cap = kBCap;
     void *comm = nullptr;        // ncclComm_t (dpg_ctx_create_comm)
     int rank = 0, nranks = 1;
+    // pinned staging arena for host -> device uploads (see upload())
+    char *stage_buf = nullptr;
+    size_t stage_cap = 0, stage_head = 0;
+    hipEvent_t stage_done = nullptr;
 };
 
 namespace {
@@ -158,6 +163,48 @@ void *ws(dpg_ctx *ctx, const char *name, size_t bytes, int *status) {
     b.bytes = want;
     return b.p;
 }
+
+// Host -> device upload of `bytes` from any host memory (stack arrays,
+// temporaries, caller buffers): the bytes are copied into a pinned arena
+// owned by the context and DMA'd from there, stream-ordered, so the source
+// may die as soon as this returns and the copy never stages pageable memory.
+// The arena is reused round-robin; when it wraps, the host waits for the
+// uploads already queued (rare: 4 MB, grown on demand).
+int upload(dpg_ctx *ctx, void *dst, const void *src, size_t bytes, hipStream_t s) {
+    if (bytes == 0) return DPG_OK;
+    const size_t need = (bytes + 255) & ~(size_t)255;
+    if (!ctx->stage_done && hipEventCreateWithFlags(&ctx->stage_done, hipEventDisableTiming) != hipSuccess)
+        return fail(ctx, DPG_ERR_HIP, "hipEventCreate (upload arena)");
+    if (need > ctx->stage_cap || ctx->stage_head + need > ctx->stage_cap) {
+        // every queued upload must have left the arena before it is reused
+        if (ctx->stage_buf && hipEventSynchronize(ctx->stage_done) != hipSuccess)
+            return fail(ctx, DPG_ERR_HIP, "hipEventSynchronize (upload arena)");
+        ctx->stage_head = 0;
+        if (need > ctx->stage_cap) {
+            if (ctx->stage_buf) (void)hipHostFree(ctx->stage_buf);
+            ctx->stage_buf = nullptr;
+            const size_t cap = std::max<size_t>(need, (size_t)4 << 20);
+            if (hipHostMalloc((void **)&ctx->stage_buf, cap, hipHostMallocDefault) != hipSuccess) {
+                ctx->stage_cap = 0;
+                return fail(ctx, DPG_ERR_OOM, "pinned upload arena");
+            }
+            ctx->stage_cap = cap;
+        }
+    }
+    char *p = ctx->stage_buf + ctx->stage_head;
+    std::memcpy(p, src, bytes);
+    ctx->stage_head += need;
+    if (hipMemcpyAsync(dst, p, bytes, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipEventRecord(ctx->stage_done, s) != hipSuccess)
+        return fail(ctx, DPG_ERR_HIP, "upload");
+    return DPG_OK;
+}
+
+#define UPLOAD(dst, src, bytes)                                  \
+    do {                                                          \
+        const int r_ = upload(ctx, (dst), (src), (bytes), s);    \
+        if (r_) return r_;                                        \
+    } while (0)
 
 #define WS(ptr, T, name, count)                                           \
     T *ptr = reinterpret_cast<T *>(ws(ctx, name, sizeof(T) * (size_t)(count), &st)); \
@@ -399,7 +446,7 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
             int64_t acc = 0;
             for (uint32_t i = 0; i < no; ++i) hout[i] = acc, acc += hc[i];
             WS(oout, int64_t, "over.out", no);
-            HIP_TRY(hipMemcpyAsync(oout, hout.data(), no * 8, hipMemcpyHostToDevice, s));
+            UPLOAD(oout, hout.data(), no * 8);
             WS(rbuf, R, "refined", std::max<int64_t>(acc, 1));
             int64_t *base2;
             uint32_t *tot2;
@@ -471,9 +518,21 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     // file, whichever binds (a static schedule must not oversubscribe)
     // one kernel per bounding family (PER_PRIVACY_ID or cross-partition), so
     // that the hot one holds one path only
+    // the cross-partition modes sort (dpg_sortb.h) when the partition key
+    // fits the sort key; PER_PRIVACY_ID, the pre-aggregate and wider keys
+    // take the hash-table kernel (dpg_wave.h).  DPG_BOUND_HASH: force it.
     auto wave_kern = per_pid ? k_bound_waves<KeyT, Item, R, true> : k_bound_waves<KeyT, Item, R, false>;
+    size_t wave_lds = WL::TOTAL;
+    bool use_sort = false;
+    if constexpr (!ItemTraits<Item>::preagg) {
+        use_sort = !per_pid && pl.pkbits <= kSkPkBits && std::getenv("DPG_BOUND_HASH") == nullptr;
+        if (use_sort) {
+            wave_kern = k_bound_sorted<Item, R>;
+            wave_lds = SortLayout<Item, R>::TOTAL;
+        }
+    }
     int wpc = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&wpc, wave_kern, 64, WL::TOTAL) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&wpc, wave_kern, 64, wave_lds) != hipSuccess ||
         wpc <= 0)
         wpc = 1;
     // waves per CU rounded down to a multiple of the 4 SIMDs: the static
@@ -481,7 +540,7 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     // sharing a SIMD next to SIMDs with one would finish last (same-box
     // A/B, config 4 with 32-KB working sets: 5 waves per CU 42 ms, 4 per
     // CU 29.7 ms)
-    int per_cu = std::min(wpc, WL::PER_CU);
+    int per_cu = std::min(wpc, (int)std::min<size_t>(16, (160 * 1024) / wave_lds));
     if (per_cu > 4) per_cu &= ~3;
     const uint32_t Gw = (uint32_t)(ctx->n_cu * per_cu);
     const uint32_t Gm = hctl.n_mchunks ? (uint32_t)std::min<uint32_t>(
@@ -516,9 +575,11 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
         bpl.phase_cyc = pc;
     }
     (void)hipFuncSetAttribute((const void *)wave_kern,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)WL::TOTAL);
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)wave_lds);
+    // zero-length marker stage: which small-chunk kernel bounded this call
+    stage(ctx, s, use_sort ? "bound.kernel=sort" : "bound.kernel=hash");
     stage(ctx, s, "bound");
-    wave_kern<<<Gw, 64, WL::TOTAL, s>>>(recs, refined, hrec, chunk_list,
+    wave_kern<<<Gw, 64, wave_lds, s>>>(recs, refined, hrec, chunk_list,
                                                           &ctl->n_chunks, bpl, items, wg_off,
                                                           wg_cnt);
     LAUNCH_CHECK();
@@ -539,9 +600,12 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     if (timing) {
         unsigned long long h[32];
         HIP_TRY(hipMemcpy(h, bpl.phase_cyc, sizeof(h), hipMemcpyDeviceToHost));
-        static const char *nmw[12] = {"A0.cas", "A1.count", "B.slots", "C1.cand", "C2.rank",
+        static const char *nmh[12] = {"A0.cas", "A1.count", "B.slots", "C1.cand", "C2.rank",
                                       "D.state", "E.mcpp", "F.acc", "G.emit", "A.probe",
                                       "Am.pidc", "Am.cand"};
+        static const char *nms[12] = {"A.pids+cand", "S.sort", "P.pairs", "M.mcpp", "F.emit",
+                                      "end", "-", "-", "-", "-", "-", "-"};
+        const char *const *nmw = use_sort ? nms : nmh;
         static const char *nmc[9] = {"A0.cas", "A1.count", "A2.barrier", "B.slots", "C.mpc",
                                      "D.state", "E.mcpp", "F.acc", "G.emit"};
         for (int part = 0; part < 2; ++part) {
@@ -590,8 +654,7 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
         }
         WS(scratch, char, "bound.scratch", total);
         WS(doff, size_t, "bound.scratch_off", n_global);
-        HIP_TRY(hipMemcpyAsync(doff, off.data(), n_global * sizeof(size_t), hipMemcpyHostToDevice,
-                               s));
+        UPLOAD(doff, off.data(), n_global * sizeof(size_t));
         BoundParams bpg = bp;
         uint32_t *gprog = watchdog_seconds() ? watchdog_buffer(n_global) : nullptr;
         bpg.progress = gprog;
@@ -803,18 +866,15 @@ int aggregate_impl(dpg_ctx *ctx, const int64_t *pid, const int64_t *pk, const do
     const int64_t P = p->n_partitions;
     WS(ctl, Control, "control", 1);
     HIP_TRY(hipMemsetAsync(ctl, 0, sizeof(Control), s));
-    {
-        Control h{};
-        h.n_scalar = n;
-        HIP_TRY(hipMemcpyAsync(&ctl->n_scalar, &h.n_scalar, 8, hipMemcpyHostToDevice, s));
-    }
+    k_set_i64<<<1, 1, 0, s>>>(&ctl->n_scalar, n);
+    LAUNCH_CHECK();
     // ---- privacy-id range
     int64_t pid_min = p->pid_min;
     uint64_t U = (uint64_t)p->pid_count;
     if (U == 0) {
         stage(ctx, s, "pidrange");
         const unsigned long long init[2] = {~0ull, 0ull};
-        HIP_TRY(hipMemcpyAsync(&ctl->pid_lo, init, 16, hipMemcpyHostToDevice, s));
+        UPLOAD(&ctl->pid_lo, init, 16);
         const int64_t blocks = std::min<int64_t>((n + 255) / 256, (int64_t)ctx->n_cu * 8);
         k_pid_minmax<<<(unsigned)blocks, 256, 0, s>>>(pid, n, &ctl->pid_lo, &ctl->pid_hi);
         LAUNCH_CHECK();
@@ -964,6 +1024,11 @@ void dpg_ctx_destroy(dpg_ctx *c) {
     for (auto &kv : c->bufs)
         if (kv.second.p) (void)hipFree(kv.second.p);
     for (auto e : c->events) (void)hipEventDestroy(e);
+    if (c->stage_done) {
+        (void)hipEventSynchronize(c->stage_done);
+        (void)hipEventDestroy(c->stage_done);
+    }
+    if (c->stage_buf) (void)hipHostFree(c->stage_buf);
     delete c;
 }
 
@@ -1099,8 +1164,7 @@ int dpg_select_and_noise(dpg_ctx *ctx, const dpg_partials *in, const dpg_select_
         if (sel->table_len <= 0 || !sel->keep_table)
             return fail(ctx, DPG_ERR_INVALID_ARG, "truncated geometric needs keep_table");
         WS(tab, double, "select.table", sel->table_len);
-        HIP_TRY(hipMemcpyAsync(tab, sel->keep_table, sizeof(double) * sel->table_len,
-                               hipMemcpyHostToDevice, s));
+        UPLOAD(tab, sel->keep_table, sizeof(double) * sel->table_len);
         a.table = tab;
     }
     NoiseArgs na{};
@@ -1203,11 +1267,11 @@ int dpg_utility_analysis(dpg_ctx *ctx, const dpg_pair_entry *pairs,
         }
     }
     WS(dcfg, UaConfig, "ua.cfg", C);
-    HIP_TRY(hipMemcpyAsync(dcfg, hc.data(), sizeof(UaConfig) * C, hipMemcpyHostToDevice, s));
+    UPLOAD(dcfg, hc.data(), sizeof(UaConfig) * C);
     a.cfg = dcfg;
     if (!tabs.empty()) {
         WS(dtab, double, "ua.tables", tabs.size());
-        HIP_TRY(hipMemcpyAsync(dtab, tabs.data(), 8 * tabs.size(), hipMemcpyHostToDevice, s));
+        UPLOAD(dtab, tabs.data(), 8 * tabs.size());
         a.tables = dtab;
     }
     a.sample_mask = u->sample_mask;
@@ -1255,7 +1319,7 @@ int dpg_utility_analysis(dpg_ctx *ctx, const dpg_pair_entry *pairs,
             ++mi;
         }
         WS(dstd, double, "ua.std", hs.size());
-        HIP_TRY(hipMemcpyAsync(dstd, hs.data(), 8 * hs.size(), hipMemcpyHostToDevice, s));
+        UPLOAD(dstd, hs.data(), 8 * hs.size());
         WS(bucket, int32_t, "ua.bucket", P);
         WS(bcount, uint32_t, "ua.bcount", kUaBuckets);
         WS(order, int64_t, "ua.order", P);
@@ -1275,7 +1339,7 @@ int dpg_utility_analysis(dpg_ctx *ctx, const dpg_pair_entry *pairs,
         HIP_TRY(hipStreamSynchronize(s));
         uint32_t run = 0, start[kUaBuckets];
         for (int b = 0; b < kUaBuckets; ++b) start[b] = run, run += hc[b];
-        HIP_TRY(hipMemcpyAsync(bcount, start, sizeof(start), hipMemcpyHostToDevice, s));
+        UPLOAD(bcount, start, sizeof(start));
         k_ua_order<<<gb, 256, 0, s>>>(a);
         LAUNCH_CHECK();
         if (run > 0) {
@@ -1322,7 +1386,7 @@ int dpg_dataset_histograms(dpg_ctx *ctx, const dpg_pair_entry *pairs, int64_t n_
     HIP_TRY(hipMemsetAsync(a.lowers, 0, 8 * (kHsBins + 1), s));
     HIP_TRY(hipMemsetAsync(pcount, 0, 4 * (size_t)P, s));
     const unsigned long long mm0[2] = {~0ull, 0ull};
-    HIP_TRY(hipMemcpyAsync(minmax, mm0, sizeof(mm0), hipMemcpyHostToDevice, s));
+    UPLOAD(minmax, mm0, sizeof(mm0));
     if (n_pairs == 0) {
         stage(ctx, s, "hist.end");
         return DPG_OK;

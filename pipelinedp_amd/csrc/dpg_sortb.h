@@ -1,0 +1,612 @@
+// dpg_sortb.h -- sort-based contribution bounding of small chunks by single
+// waves (gfx950): the default bounding kernel of the cross-partition modes.
+//
+// A small chunk (<= kWCap = 512 records of <= kWCq = 128 privacy-id hash
+// slots, dpg_chunk.h) is bounded by one 64-lane wave that owns a private LDS
+// working set.  Instead of a hash table of pairs (dpg_wave.h) the wave SORTS
+// the chunk's candidate records in registers by the key the reference's
+// sampler orders pairs by (contribution_bounders.py:90-92; oracle
+// dp_oracle.c: key = pair_priority << 32 | pk per privacy id):
+//
+//   skey = pid slot q (7 bits) | pair priority pp (32 bits) | pk (24 bits)
+//
+// so that the records of one pair are adjacent, the pairs of one privacy id
+// follow each other in ascending (pp, pk) order, and a pair is kept iff
+// fewer than mpc pairs of its privacy id precede it -- a segmented count
+// over the sorted sequence instead of hash inserts, probing and a per-pid
+// threshold search.  Per chunk:
+//
+//   A  records per pid slot (LDS atomics), pid hash and candidate bound of
+//      every occupied slot: a pid with more than mpc records only sends the
+//      records whose pair priority is below a bound aimed at ~CAND x (mpc +
+//      2 sqrt(mpc) + 2) records (a pair's records share its priority, so
+//      whole pairs pass or fail); candidates are compacted into LDS
+//   S  bitonic sort of the candidates' (skey, ordinal) in registers: E =
+//      1, 2, 4 or 8 elements per lane (64 E >= candidates), cross-lane steps
+//      by DPP / ds_swizzle / bpermute
+//   P  pair starts, pair ordinals (wave scan), pair rank inside the pid; a
+//      filtered pid that shows fewer than mpc candidate pairs restarts the
+//      chunk with all of its records (rare); a pair is kept iff rank < mpc
+//   M  records of kept pairs gather their values; pairs over mcpp rank their
+//      records by record priority (contribution_bounders.py:74-76) inside
+//      the pair's segment
+//   F  clipped accumulators (combiners.py:255-500) per pair in LDS; one Item
+//      per kept pair.
+//
+// Kept sets are bit-identical to the oracle's: the order is the oracle's
+// key order whenever pk < 2^24 (the host uses the hash kernel otherwise).
+// PER_PRIVACY_ID bounding and the utility pre-aggregate keep dpg_wave.h.
+#pragma once
+
+#include "dpg_wave.h"
+
+namespace dpg {
+
+// candidate bound of the sort kernel (records per pid aimed at, times
+// mpc + 2 sqrt(mpc) + 2); the sort makes extra candidates cheap, restarts
+// (a pid short of mpc candidate pairs) cost a second sort
+#ifndef DPG_SORT_CAND_C
+#define DPG_SORT_CAND_C 2.0f
+#endif
+
+constexpr uint32_t kSkPkBits = 24;  // partition-key bits of the sort key
+constexpr uint64_t kSkPad = ~0ull;  // padding elements (real keys have bit 63 clear)
+
+template <class Item, class R>
+struct SortLayout {
+    static constexpr int NACC = ItemTraits<Item>::var ? (ItemTraits<Item>::sum ? 3 : 2) : 1;
+    static constexpr size_t PIDC = 0;                  // records per pid slot
+    static constexpr size_t PIDV = PIDC + 4 * kWCq;    // pid hash
+    static constexpr size_t CBND = PIDV + 4 * kWCq;    // candidate bound
+    static constexpr size_t PBASE = CBND + 4 * kWCq;   // ordinal of the pid's first pair
+    static constexpr size_t FULL = PBASE + 4 * kWCq;   // pid shows >= mpc candidate pairs
+    static constexpr size_t CKEY = FULL + 4 * kWCq;    // candidate keys; after the sort
+                                                       // the record keys by position
+    static constexpr size_t RECS = CKEY + 8 * kWCap;   // the chunk's records by position
+    static constexpr size_t CORD = RECS + a16(sizeof(R) * kWCap);  // candidate -> position
+    static constexpr size_t PSTART = CORD + a16(2 * kWCap);        // first position per pair
+    static constexpr size_t ACC = PSTART + a16(4 * (kWCap + 1));
+    static constexpr size_t END = ACC + 8 * kWCap * NACC;
+    static constexpr size_t TOTAL = (END + 4095) & ~(size_t)4095;
+    static_assert(TOTAL <= 40 * 1024, "sort working set too large");
+};
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o, 64));
+    return x;
+}
+
+// x of lane (lane ^ m), m < 64 either a power of two or 2^t - 1: quad DPP
+// for 1, 2, 3, half-row / row mirrors for 7 and 15, the ds_swizzle bit-mask
+// mode inside 32 lanes for 4, 8, 16 and 31, bpermute for 32 and 63.  The
+// callers' loops are fully unrolled, so m is a constant and one case stays.
+__device__ __forceinline__ uint32_t xlane(uint32_t x, int m) {
+    switch (m) {
+        case 1:
+            return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);  // [1,0,3,2]
+        case 2:
+            return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);  // [2,3,0,1]
+        case 3:
+            return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x1B, 0xF, 0xF, false);  // [3,2,1,0]
+        case 7:
+            return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, false);  // half mirror
+        case 15:
+            return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x140, 0xF, 0xF, false);  // row mirror
+        case 4:
+            return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x101F);
+        case 8:
+            return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x201F);
+        case 16:
+            return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x401F);
+        case 31:
+            return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x7C1F);
+        default:
+            return (uint32_t)__shfl_xor((int)x, m, 64);
+    }
+}
+__device__ __forceinline__ uint64_t xlane64(uint64_t x, int m) {
+    return ((uint64_t)xlane((uint32_t)(x >> 32), m) << 32) | xlane((uint32_t)x, m);
+}
+
+// Ascending sort of 64 E (key, payload) elements, element i = lane E + j in
+// k[j], o[j]: a bitonic network in the form whose comparators all put the
+// minimum at the lower index -- each merge of block size kk first compares
+// i with its mirror i ^ (kk - 1), then half-cleans with i ^ s.  Steps inside
+// a lane's E elements need no exchange; the others read the partner lane's
+// element through xlane.  The only lane-dependent decision is "is this the
+// lower index", one lane bit.  Equal keys never move, so partners agree.
+template <int E>
+__device__ __forceinline__ void bitonic_sort(uint64_t (&k)[E], uint32_t (&o)[E]) {
+    constexpr int LOG_S = E == 1 ? 6 : E == 2 ? 7 : E == 4 ? 8 : 9;
+    constexpr int LOG_E = LOG_S - 6;
+    // a fresh copy per call: keeps the lane-bit masks from being hoisted out
+    // of the chunk loop (they would live in scalar registers all along)
+    uint32_t lid = __lane_id();
+    asm volatile("" : "+v"(lid));
+    auto cex = [&](int j, int j2) {  // in-lane compare-exchange, min to j
+        const bool sw = k[j] > k[j2];
+        const uint64_t a = k[j], b = k[j2];
+        const uint32_t oa = o[j], ob = o[j2];
+        k[j] = sw ? b : a;
+        k[j2] = sw ? a : b;
+        o[j] = sw ? ob : oa;
+        o[j2] = sw ? oa : ob;
+    };
+#pragma unroll
+    for (int lk = 1; lk <= LOG_S; ++lk) {
+        const int kk = 1 << lk;
+        // mirror step
+        if (lk <= LOG_E) {
+#pragma unroll
+            for (int j = 0; j < E; ++j) {
+                const int j2 = j ^ (kk - 1);
+                if (j < j2) cex(j, j2);
+            }
+        } else {
+            const int m = (kk >> LOG_E) - 1;            // partner lane = lane ^ m, slot E-1-j
+            const bool lower = (lid & (uint32_t)((m + 1) >> 1)) == 0;
+            uint64_t y[E];
+            uint32_t yo[E];
+#pragma unroll
+            for (int j = 0; j < E; ++j) {
+                y[j] = xlane64(k[E - 1 - j], m);
+                yo[j] = xlane(o[E - 1 - j], m);
+            }
+#pragma unroll
+            for (int j = 0; j < E; ++j) {
+                const bool take = lower ? (y[j] < k[j]) : (y[j] > k[j]);
+                k[j] = take ? y[j] : k[j];
+                o[j] = take ? yo[j] : o[j];
+            }
+        }
+        // half-cleaners
+#pragma unroll
+        for (int ls = lk - 2; ls >= 0; --ls) {
+            const int sd = 1 << ls;
+            if (ls < LOG_E) {
+#pragma unroll
+                for (int j = 0; j < E; ++j)
+                    if (!(j & sd)) cex(j, j | sd);
+            } else {
+                const int m = sd >> LOG_E;
+                const bool lower = (lid & (uint32_t)m) == 0;
+#pragma unroll
+                for (int j = 0; j < E; ++j) {
+                    const uint64_t y = xlane64(k[j], m);
+                    const uint32_t yo = xlane(o[j], m);
+                    const bool take = lower ? (y < k[j]) : (y > k[j]);
+                    k[j] = take ? y : k[j];
+                    o[j] = take ? yo : o[j];
+                }
+            }
+        }
+    }
+}
+
+// Sorts the nc candidates and bounds them (phases S, P, M, F of the header).
+// Returns false when the chunk must restart: the filtered pids short of mpc
+// candidate pairs have had their bound lifted (their CBND set to all-pass).
+// Per-element flags live in per-lane bit masks (bit j = element j).
+template <class Item, class R, int E>
+__device__ __forceinline__ bool sort_chunk(uint32_t nc, char *smem, const BoundParams &bp,
+                                           bool last_round, uint32_t hbound, uint32_t hidx,
+                                           Item *items, uint32_t &nitems, PhaseTimer &clk) {
+    using L = SortLayout<Item, R>;
+    constexpr bool kVar = ItemTraits<Item>::var;
+    constexpr bool kSum = ItemTraits<Item>::sum;
+    uint32_t *pidv = reinterpret_cast<uint32_t *>(smem + L::PIDV);
+    uint32_t *pidc = reinterpret_cast<uint32_t *>(smem + L::PIDC);
+    uint32_t *cbnd = reinterpret_cast<uint32_t *>(smem + L::CBND);
+    uint32_t *pbase = reinterpret_cast<uint32_t *>(smem + L::PBASE);
+    uint32_t *full = reinterpret_cast<uint32_t *>(smem + L::FULL);
+    uint64_t *ckey = reinterpret_cast<uint64_t *>(smem + L::CKEY);
+    uint64_t *rks = ckey;  // after the sort
+    const R *recl = reinterpret_cast<const R *>(smem + L::RECS);
+    const uint16_t *cord = reinterpret_cast<const uint16_t *>(smem + L::CORD);
+    uint32_t *pstart = reinterpret_cast<uint32_t *>(smem + L::PSTART);
+    double *acc = reinterpret_cast<double *>(smem + L::ACC);
+    double *acc_nsum = acc + (kSum ? kWCap : 0);
+    double *acc_nsq = acc_nsum + kWCap;
+    const uint32_t lane = __lane_id();
+    const Fmt f = bp.fmt;
+    const bool need_v = bp.need_values != 0;
+    const bool cap_pp = bp.mode == DPG_MODE_CROSS_AND_PER_PARTITION;
+    const bool sample = cap_pp && need_v;
+    const bool part_clip = bp.sum_mode == DPG_SUM_CLIP_PARTITION;
+    constexpr uint32_t kPkMask = (1u << kSkPkBits) - 1u;
+
+    // ---- S: sort (key, record position)
+    uint64_t k[E];
+    uint32_t o[E];
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+        const uint32_t i = lane * E + j;
+        const uint32_t ic = min(i, (uint32_t)kWCap - 1);
+        const uint64_t x = ckey[ic];
+        const uint32_t y = cord[ic];
+        k[j] = i < nc ? x : kSkPad;
+        o[j] = i < nc ? y : 0u;
+    }
+    full[lane] = 0;
+    full[lane + 64u] = 0;
+    bitonic_sort<E>(k, o);
+    mark(bp, 1, clk);
+
+    // ---- P: pair starts, ordinals, rank inside the pid
+    const uint64_t prev_last = (uint64_t)__shfl_up((long long)k[E - 1], 1, 64);
+    uint32_t validm = 0, psm = 0, pidm = 0;
+    uint32_t a[E];
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+        const uint32_t i = lane * E + j;
+        const uint64_t pv = j ? k[j - 1] : prev_last;
+        const bool val = i < nc;
+        const bool p = val && (i == 0 || k[j] != pv);
+        const bool d = val && (i == 0 || (k[j] >> 56) != (pv >> 56));
+        validm |= val ? 1u << j : 0u;
+        psm |= p ? 1u << j : 0u;
+        pidm |= d ? 1u << j : 0u;
+        cnt += p ? 1u : 0u;
+        a[j] = cnt;  // inclusive within the lane
+    }
+    uint32_t npairs;
+    const uint32_t before = wave_excl_scan(cnt, npairs) - 1u;
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+        a[j] += before;  // pair ordinal
+        if ((psm >> j) & 1u) pstart[a[j]] = lane * E + j;
+        if ((pidm >> j) & 1u) pbase[(uint32_t)(k[j] >> 56) & (kWCq - 1)] = a[j];
+    }
+    if (lane == 0) pstart[npairs] = nc;
+    wave_sync();
+    uint32_t kpm = 0;
+    {
+        uint32_t pb[E];
+#pragma unroll
+        for (int j = 0; j < E; ++j) pb[j] = pbase[(uint32_t)(k[j] >> 56) & (kWCq - 1)];
+#pragma unroll
+        for (int j = 0; j < E; ++j) {
+            const uint32_t rank = a[j] - pb[j];
+            if (((psm >> j) & 1u) && rank == bp.mpc - 1)
+                full[(uint32_t)(k[j] >> 56) & (kWCq - 1)] = 1u;
+            kpm |= (((validm >> j) & 1u) && rank < bp.mpc) ? 1u << j : 0u;
+        }
+    }
+    wave_sync();
+    // pids filtered by their bound that show fewer than mpc candidate pairs
+    // may own kept pairs above the bound
+    {
+        bool shrt = false;
+#pragma unroll
+        for (int jj = 0; jj < (int)(kWCq / 64); ++jj) {
+            const uint32_t qq = lane + 64u * jj;
+            const bool sh = pidc[qq] > 0 && cbnd[qq] != 0xFFFFFFFFu && full[qq] == 0;
+            if (sh && !hbound) cbnd[qq] = 0xFFFFFFFFu;
+            shrt |= sh;
+        }
+        if (__ballot(shrt) && !last_round) {
+            wave_sync();
+            if (hbound) {
+                // a heavy chunk holds only its pid's candidates: the bucket
+                // goes back to the global-memory kernel (rare)
+                if (lane == 0) bp.heavy_fb[atomicAdd(bp.heavy_nfb, 1u)] = hidx;
+                return true;
+            }
+            return false;
+        }
+    }
+    mark(bp, 2, clk);
+
+    // ---- M: kept pairs; values of their records; mcpp sample of over-full
+    // pairs by record priority
+    uint32_t st[E], len[E], idx[E];
+    double v[E];
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+        st[j] = pstart[min(a[j], (uint32_t)kWCap - 1)];
+        len[j] = pstart[min(a[j] + 1, (uint32_t)kWCap)];
+        idx[j] = RecOps<R>::idx(recl[min(o[j], (uint32_t)kWCap - 1)], f);
+    }
+    uint32_t overm = 0, maxlen = 0;
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+        len[j] -= st[j];
+        const bool kp = (kpm >> j) & 1u;
+        const bool ov = sample && kp && len[j] > bp.mcpp;
+        overm |= ov ? 1u << j : 0u;
+        maxlen = max(maxlen, ov ? len[j] : 0u);
+        v[j] = (need_v && kp) ? bp.value[idx[j]] : 0.0;
+    }
+    uint32_t keepm = kpm;
+    maxlen = __builtin_amdgcn_readfirstlane(wave_max_u32(maxlen));
+    if (maxlen) {
+        // record keys of over-full kept pairs, by sorted position; a record
+        // is kept iff fewer than mcpp keys of its pair are smaller
+#pragma unroll
+        for (int j = 0; j < E; ++j) {
+            if (!((overm >> j) & 1u)) continue;
+            const uint32_t q = (uint32_t)(k[j] >> 56) & (kWCq - 1);
+            rks[lane * E + j] = rec_prio_h(pidv[q], (uint32_t)k[j] & kPkMask,
+                                           (uint64_t)(bp.rec_base + idx[j]));
+        }
+        wave_sync();
+#pragma unroll
+        for (int j = 0; j < E; ++j) {
+            if (!__ballot((overm >> j) & 1u)) continue;
+            const bool ov = (overm >> j) & 1u;
+            const uint64_t mine = rks[lane * E + j];
+            const uint32_t lm = max(len[j], 1u) - 1u;
+            uint32_t below = 0;
+            for (uint32_t t = 0; t < maxlen; t += 2) {
+                const uint64_t y0 = rks[min(st[j] + min(t, lm), (uint32_t)kWCap - 1)];
+                const uint64_t y1 = rks[min(st[j] + min(t + 1, lm), (uint32_t)kWCap - 1)];
+                below += (t < len[j] && y0 < mine) ? 1u : 0u;
+                below += (t + 1 < len[j] && y1 < mine) ? 1u : 0u;
+            }
+            if (ov && below >= bp.mcpp) keepm &= ~(1u << j);
+        }
+    }
+    mark(bp, 3, clk);
+
+    // ---- F: accumulators of kept records, one item per kept pair
+    const uint32_t em = psm & kpm;
+    if (need_v) {
+#pragma unroll
+        for (int j = 0; j < E; ++j) {
+            if (!((em >> j) & 1u)) continue;
+            if (kSum) acc[a[j]] = 0.0;
+            if (kVar) {
+                acc_nsum[a[j]] = 0.0;
+                acc_nsq[a[j]] = 0.0;
+            }
+        }
+        wave_sync();
+#pragma unroll
+        for (int j = 0; j < E; ++j) {
+            if (!((keepm >> j) & 1u)) continue;
+            if (part_clip) {
+                atomicAdd(&acc[a[j]], v[j]);
+            } else {
+                const double x = clampd(v[j], bp.lo, bp.hi);
+                if (kSum) atomicAdd(&acc[a[j]], x);
+                if (kVar) {
+                    const double y = x - bp.mid;
+                    atomicAdd(&acc_nsum[a[j]], y);
+                    atomicAdd(&acc_nsq[a[j]], y * y);
+                }
+            }
+        }
+        wave_sync();
+    }
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+        const bool e = (em >> j) & 1u;
+        const uint64_t be = __ballot(e);
+        if (e) {
+            Item it;
+            it.pk = (uint32_t)k[j] & kPkMask;
+            it.cnt = cap_pp ? min(len[j], bp.mcpp) : len[j];
+            if constexpr (kSum) {
+                const double s = need_v ? acc[a[j]] : 0.0;
+                it.sum = (need_v && part_clip) ? clampd(s, bp.lo_pp, bp.hi_pp) : s;
+            }
+            if constexpr (kVar) {
+                it.nsum = need_v ? acc_nsum[a[j]] : 0.0;
+                it.nsq = need_v ? acc_nsq[a[j]] : 0.0;
+            }
+            items[nitems + lanes_below(be)] = it;
+        }
+        nitems += (uint32_t)__popcll(be);
+    }
+    mark(bp, 4, clk);
+    return true;
+}
+
+// One small chunk: pid counts, pid hashes and candidate bounds, candidate
+// compaction, then sort_chunk (a second round with the short pids' bounds
+// lifted when the first finds one).
+template <class Item, class R>
+__device__ __forceinline__ uint32_t sort_bound_chunk(const R (&r)[kWRPT], uint32_t n, uint32_t d1,
+                                                     uint32_t hbase, char *smem,
+                                                     const BoundParams &bp, Item *items,
+                                                     uint32_t nitems, PhaseTimer &clk,
+                                                     uint32_t hbound, uint32_t hidx) {
+    using L = SortLayout<Item, R>;
+    uint32_t *pidv = reinterpret_cast<uint32_t *>(smem + L::PIDV);
+    uint32_t *pidc = reinterpret_cast<uint32_t *>(smem + L::PIDC);
+    uint32_t *cbnd = reinterpret_cast<uint32_t *>(smem + L::CBND);
+    uint64_t *ckey = reinterpret_cast<uint64_t *>(smem + L::CKEY);
+    R *recl = reinterpret_cast<R *>(smem + L::RECS);
+    uint16_t *cord = reinterpret_cast<uint16_t *>(smem + L::CORD);
+    uint32_t *olist = reinterpret_cast<uint32_t *>(smem + L::PSTART);
+    const uint32_t lane = __lane_id();
+    const Fmt f = bp.fmt;
+    const uint32_t pkb = f.pkbits;
+    const uint64_t pkmask = (1ull << pkb) - 1ull;
+    const uint32_t hshift = f.kbits - f.b1;
+    const uint32_t kn = (n + 63) >> 6;  // occupied record slots per lane (uniform)
+
+    // ---- A: records to LDS; records per pid slot
+    uint64_t sk[kWRPT];  // q << 56 | pk (pair priority added below)
+    uint32_t validm = 0;
+#pragma unroll
+    for (int k = 0; k < kWRPT && k < (int)kn; ++k) {
+        validm |= lane + 64u * k < n ? 1u << k : 0u;
+        const uint64_t key = RecOps<R>::key(r[k], f);
+        const uint32_t q = ((uint32_t)(key >> pkb) - hbase) & (kWCq - 1);
+        sk[k] = ((uint64_t)q << 56) | (key & pkmask);
+        recl[lane + 64u * k] = r[k];
+    }
+#pragma unroll
+    for (int k = 0; k < kWRPT && k < (int)kn; ++k)
+        if ((validm >> k) & 1u) atomicAdd(&pidc[(uint32_t)(sk[k] >> 56)], 1u);
+    wave_sync();
+    // pid hash and candidate bound of the occupied slots (compacted)
+    {
+        const float cmul = DPG_SORT_CAND_C * ((float)bp.mpc + 2.0f * sqrtf((float)bp.mpc) + 2.0f);
+        uint32_t nocc = 0;
+#pragma unroll
+        for (int j = 0; j < (int)(kWCq / 64); ++j) {
+            const uint32_t qq = lane + 64u * j;
+            const bool occ = pidc[qq] > 0;
+            const uint64_t bo = __ballot(occ);
+            if (occ) olist[nocc + lanes_below(bo)] = qq;
+            nocc += (uint32_t)__popcll(bo);
+        }
+        wave_sync();
+        for (uint32_t o = 0; o < nocc; o += 64) {
+            if (o + lane < nocc) {
+                const uint32_t qq = olist[o + lane];
+                pidv[qq] = pid_hash(bp.seed, (uint64_t)(bp.pid_min + (int64_t)hk_inv(
+                                                            (d1 << hshift) | (hbase + qq), bp.hash)));
+                const uint32_t rc = pidc[qq];
+                const float fr = cmul / (float)rc;
+                cbnd[qq] = hbound ? hbound
+                                  : (rc <= bp.mpc || fr >= 1.0f ? 0xFFFFFFFFu
+                                                                : (uint32_t)(fr * 4294967296.0f));
+            }
+        }
+    }
+    wave_sync();
+    {
+        uint32_t pv[kWRPT];
+#pragma unroll
+        for (int k = 0; k < kWRPT && k < (int)kn; ++k) pv[k] = pidv[(uint32_t)(sk[k] >> 56)];
+#pragma unroll
+        for (int k = 0; k < kWRPT && k < (int)kn; ++k)
+            sk[k] |= (uint64_t)pair_prio_h(pv[k], (uint32_t)sk[k]) << kSkPkBits;
+    }
+    mark(bp, 0, clk);
+    for (uint32_t round = 0;; ++round) {
+        // ---- candidates (pair priority within the pid's bound), compacted
+        uint32_t cb[kWRPT];
+#pragma unroll
+        for (int k = 0; k < kWRPT && k < (int)kn; ++k) cb[k] = cbnd[(uint32_t)(sk[k] >> 56)];
+        uint32_t nc = 0;
+#pragma unroll
+        for (int k = 0; k < kWRPT && k < (int)kn; ++k) {
+            const bool c = ((validm >> k) & 1u) && (uint32_t)(sk[k] >> kSkPkBits) <= cb[k];
+            const uint64_t bc = __ballot(c);
+            if (c) {
+                const uint32_t e = nc + lanes_below(bc);
+                ckey[e] = sk[k];
+                cord[e] = (uint16_t)(lane + 64u * k);
+            }
+            nc += (uint32_t)__popcll(bc);
+        }
+        wave_sync();
+        const bool last = round > 0;
+        bool done;
+        if (nc <= 64)
+            done = sort_chunk<Item, R, 1>(nc, smem, bp, last, hbound, hidx, items, nitems, clk);
+        else if (nc <= 128)
+            done = sort_chunk<Item, R, 2>(nc, smem, bp, last, hbound, hidx, items, nitems, clk);
+        else if (nc <= 256)
+            done = sort_chunk<Item, R, 4>(nc, smem, bp, last, hbound, hidx, items, nitems, clk);
+        else
+            done = sort_chunk<Item, R, 8>(nc, smem, bp, last, hbound, hidx, items, nitems, clk);
+        wave_sync();
+        if (done) break;
+    }
+#pragma unroll
+    for (int j = 0; j < (int)(kWCq / 64); ++j) pidc[lane + 64u * j] = 0;
+    wave_sync();
+    mark(bp, 5, clk);
+    return nitems;
+}
+
+// Persistent single-wave workgroups walk the small-chunk list statically
+// (w, w + G, ...), as k_bound_waves; workgroup g appends its items to
+// items[wg_off[g], ...) and leaves the count in wg_cnt[g].
+template <class Item, class R>
+__global__ __launch_bounds__(64, 2) void k_bound_sorted(const R *recs, const R *refined,
+                                                        const R *heavy, const uint4 *chunks,
+                                                        const uint32_t *n_chunks, BoundParams bp,
+                                                        Item *items, const int64_t *wg_off,
+                                                        uint32_t *wg_cnt) {
+    using L = SortLayout<Item, R>;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    PhaseTimer clk;
+    timer_start(bp, clk);
+    // parameters used in one phase each: vector registers (see vreg; the
+    // kernel is short of scalar registers, not of vector ones)
+    bp.lo = vreg(bp.lo);
+    bp.hi = vreg(bp.hi);
+    bp.lo_pp = vreg(bp.lo_pp);
+    bp.hi_pp = vreg(bp.hi_pp);
+    bp.mid = vreg(bp.mid);
+    bp.seed = vreg(bp.seed);
+    bp.pid_min = vreg(bp.pid_min);
+    bp.rec_base = vreg(bp.rec_base);
+    bp.hash.mask = vreg(bp.hash.mask);
+    bp.hash.i1 = vreg(bp.hash.i1);
+    bp.hash.i2 = vreg(bp.hash.i2);
+    bp.mpc = vreg(bp.mpc);
+    bp.mcpp = vreg(bp.mcpp);
+    bp.fmt.ib = vreg(bp.fmt.ib);
+    bp.fmt.pkbits = vreg(bp.fmt.pkbits);
+    bp.fmt.kbits = vreg(bp.fmt.kbits);
+    bp.fmt.b1 = vreg(bp.fmt.b1);
+    bp.value = vreg(bp.value);
+    bp.heavy_fb = vreg(bp.heavy_fb);
+    bp.heavy_nfb = vreg(bp.heavy_nfb);
+    const uint32_t nch = __builtin_amdgcn_readfirstlane(*n_chunks);
+    Item *my_items = items + wg_off[blockIdx.x];
+    const uint32_t lane = __lane_id();
+    {
+        uint32_t *pidc = reinterpret_cast<uint32_t *>(smem + L::PIDC);
+        for (uint32_t i = lane; i < kWCq; i += 64) pidc[i] = 0;
+    }
+    wave_sync();
+    R r[kWRPT], rn[kWRPT];
+    const uint32_t G = gridDim.x;
+    uint32_t w = blockIdx.x;
+    uint32_t n = 0, d1 = 0, hb = 0, hbound = 0, hidx = 0, nitems = 0;
+    uint4 dn = make_uint4(0, 0, 0, 0);
+    if (w < nch) {
+        const uint4 d = make_uint4(__builtin_amdgcn_readfirstlane(chunks[w].x),
+                                   __builtin_amdgcn_readfirstlane(chunks[w].y),
+                                   __builtin_amdgcn_readfirstlane(chunks[w].z),
+                                   __builtin_amdgcn_readfirstlane(chunks[w].w));
+        n = d.y & kChunkCount;
+        d1 = d.z & 0xFFFFu;
+        hb = d.w;
+        hbound = heavy_bound(d);
+        hidx = d.x / (uint32_t)kWCap;
+        const R *b = wave_chunk_base(d, recs, refined, heavy);
+#pragma unroll
+        for (int k = 0; k < kWRPT; ++k) r[k] = b[min(lane + 64u * k, n - 1)];
+        if (w + G < nch) dn = chunks[w + G];
+    }
+    for (; w < nch; w += G) {
+        uint4 dnn = make_uint4(0, 0, 0, 0);
+        if (w + 2 * G < nch) dnn = chunks[w + 2 * G];
+        const uint4 du = make_uint4(__builtin_amdgcn_readfirstlane(dn.x),
+                                    __builtin_amdgcn_readfirstlane(dn.y),
+                                    __builtin_amdgcn_readfirstlane(dn.z),
+                                    __builtin_amdgcn_readfirstlane(dn.w));
+        const uint32_t nn = du.y & kChunkCount;
+        // the next chunk's records load while this one is processed
+        if (nn > 0) {
+            const R *nb = wave_chunk_base(du, recs, refined, heavy);
+#pragma unroll
+            for (int k = 0; k < kWRPT; ++k) rn[k] = nb[min(lane + 64u * k, nn - 1)];
+        }
+        nitems = sort_bound_chunk<Item, R>(r, n, d1, hb, smem, bp, my_items, nitems, clk, hbound,
+                                           hidx);
+#pragma unroll
+        for (int k = 0; k < kWRPT; ++k) r[k] = rn[k];
+        n = nn;
+        d1 = du.z & 0xFFFFu;
+        hb = du.w;
+        hbound = heavy_bound(du);
+        hidx = du.x / (uint32_t)kWCap;
+        dn = dnn;
+    }
+    if (lane == 0) wg_cnt[blockIdx.x] = nitems;
+    timer_flush(bp, clk);
+}
+
+}  // namespace dpg

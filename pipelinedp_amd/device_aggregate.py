@@ -7,7 +7,8 @@ object keeps that contract: nothing touches the GPU until the first
 `__iter__` / `materialize()`, and budgets are read at that moment.
 
 Device pipeline per call (include/dpg.h):
-  dpg_bound_aggregate -> [multi-GPU: reduce-scatter of the dense partials]
+  dpg_bound_aggregate -> [multi-GPU: reduce-scatter of the dense partials,
+  or an all-to-all of the occupied ones: distributed.exchange_partials]
   -> dpg_select_and_noise -> dpg_compact_kept.
 """
 import ctypes
@@ -77,6 +78,7 @@ class DeviceAggregation:
         # release; multi-GPU releases broadcast rank 0's.
         self.nonce: Optional[int] = None
         self.last_bound_fields: Optional[dict] = None
+        self.last_exchange: Optional[dict] = None
         self.last_select_fields: Optional[dict] = None
 
     # ------------------------------------------------------------ public
@@ -204,9 +206,10 @@ class DeviceAggregation:
             self.last_partials = tensors
             pk_offset, local_P = 0, P
             public_mask_local = enc.public_mask
+            self.last_exchange = None
             if backend.world_size > 1:
-                tensors, pk_offset, local_P = distributed.reduce_scatter_partials(
-                    tensors, P, backend.process_group)
+                tensors, pk_offset, local_P, self.last_exchange = distributed.exchange_partials(
+                    tensors, P, backend.process_group, backend.exchange)
                 if public_mask_local is not None:
                     public_mask_local = distributed.slice_bitmap(
                         enc.public_mask, pk_offset, local_P)

@@ -2,13 +2,22 @@
 
 Records are sharded by privacy id before they reach a rank (each privacy id
 lives on exactly one GPU), so contribution bounding is shard-local and the
-only exchange is the merge of the dense per-partition partials: ONE
-`reduce_scatter` (sum) of all accumulator arrays packed together gives every
-rank an equal, contiguous slice of the partition space; the owner runs
+only exchange is the merge of the per-partition partials.  Every rank owns
+an equal, contiguous slice of the partition space; the owner runs
 selection + noise for its slice, and the kept results are all-gathered.
+Two exchanges reach that slice:
 
-Over RCCL/xGMI that is one reduce-scatter of 8 B x P x (number of
-accumulator arrays) per release (P = 1e6, COUNT+SUM+PID: 24 MB).  The
+* dense -- ONE `reduce_scatter` (sum) of all accumulator arrays packed
+  together: 8 B x P x A per rank (A = accumulator arrays; P = 1e6,
+  COUNT+SUM+PID: 24 MB), whatever the occupancy;
+* sparse -- ONE `all_to_all` of the occupied partitions only, as rows
+  (pk, partial_1..A) routed to the rank owning pk: 8 B x (1 + A) x nnz per
+  rank (nnz = partitions with a kept pair on that rank), after a
+  world-sized count exchange.  Config 4 (P = 1e8, ~1e7 occupied) moves
+  ~0.5 GB instead of 4 GB per rank.
+
+`exchange_partials` picks the cheaper one from the largest nnz over ranks
+(one all_reduce of a scalar, so every rank takes the same branch).  The
 integer accumulators travel as float64, which is exact below 2^53 (a rank
 holds < 2^32 records, so no count comes near it).  With gloo (CPU tests,
 and several ranks sharing one GPU) the collectives are staged through host
@@ -85,6 +94,97 @@ def reduce_scatter_partials(tensors: Dict[str, Optional[torch.Tensor]], P: int, 
         out[k] = (col.round().to(torch.int64) if tensors[k].dtype == torch.int64
                   else col).contiguous()
     return out, lo, n_local
+
+
+def _names(tensors) -> list:
+    return [k for k in _PACK_ORDER if tensors.get(k) is not None]
+
+
+def exchange_bytes(P: int, nnz: int, n_arrays: int) -> Dict[str, int]:
+    """Bytes one rank contributes to each exchange (the send side)."""
+    return {"reduce_scatter": 8 * n_arrays * P, "all_to_all": 8 * (1 + n_arrays) * nnz}
+
+
+def choose_exchange(rows: torch.Tensor, P: int, n_arrays: int, group, mode: str = "auto"
+                    ) -> Tuple[str, int]:
+    """The exchange every rank of `group` uses, and the largest occupancy
+    over ranks.  'auto' takes the sparse all-to-all when its rows are at
+    most half the dense reduce-scatter's bytes (the count exchange and the
+    host round trip for the split sizes cost latency the dense path does
+    not pay)."""
+    if mode not in ("auto", "reduce_scatter", "all_to_all"):
+        raise ValueError(f"unknown exchange {mode!r}")
+    nnz = int(torch.count_nonzero(rows).item())
+    dev = rows.device if _is_nccl(group) else torch.device("cpu")
+    t = torch.tensor([nnz], dtype=torch.int64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    nnz_max = int(t.item())
+    if mode != "auto":
+        return mode, nnz_max
+    b = exchange_bytes(P, nnz_max, n_arrays)
+    return ("all_to_all" if 2 * b["all_to_all"] <= b["reduce_scatter"] else "reduce_scatter",
+            nnz_max)
+
+
+def all_to_all_partials(tensors: Dict[str, Optional[torch.Tensor]], P: int, group
+                        ) -> Tuple[Dict[str, Optional[torch.Tensor]], int, int]:
+    """Sparse merge: the occupied partitions (rows > 0) of every rank travel
+    as (pk, partials...) rows to the rank owning pk's slice; the owner adds
+    them into its dense slice, source rank by source rank (pks are unique
+    within one source, so every add is conflict-free and the merge is
+    deterministic).  Same result as reduce_scatter_partials."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    chunk = (P + world - 1) // world
+    lo, n_local = slice_bounds(P, world, rank)
+    names = _names(tensors)
+    dev = tensors[names[0]].device
+    nccl = _is_nccl(group)
+    cdev = dev if nccl else torch.device("cpu")
+    idx = torch.nonzero(tensors["rows"]).flatten()  # ascending, so grouped by owner
+    send = torch.empty((idx.numel(), 1 + len(names)), dtype=torch.float64, device=dev)
+    send[:, 0] = idx.to(torch.float64)
+    for j, k in enumerate(names):
+        send[:, 1 + j] = tensors[k][idx].to(torch.float64)
+    send_counts = torch.bincount(idx // chunk, minlength=world).to(torch.int64)
+    recv_counts = torch.empty_like(send_counts, device=cdev)
+    dist.all_to_all_single(recv_counts, send_counts.to(cdev), group=group)
+    sc, rc = send_counts.tolist(), recv_counts.tolist()
+    recv = torch.empty((sum(rc), 1 + len(names)), dtype=torch.float64, device=cdev)
+    dist.all_to_all_single(recv, send.to(cdev), output_split_sizes=rc, input_split_sizes=sc,
+                           group=group)
+    recv = recv.to(dev)
+    acc = torch.zeros((len(names), n_local), dtype=torch.float64, device=dev)
+    o = 0
+    for c in rc:  # source rank order
+        if c:
+            blk = recv[o:o + c]
+            li = blk[:, 0].round().to(torch.int64) - lo
+            acc[:, li] += blk[:, 1:].t()
+        o += c
+    out: Dict[str, Optional[torch.Tensor]] = {k: None for k in _PACK_ORDER}
+    for j, k in enumerate(names):
+        col = acc[j]
+        out[k] = (col.round().to(torch.int64) if tensors[k].dtype == torch.int64
+                  else col).contiguous()
+    return out, lo, n_local
+
+
+def exchange_partials(tensors: Dict[str, Optional[torch.Tensor]], P: int, group,
+                      mode: str = "auto"):
+    """Merges the partials of every rank into this rank's slice with the
+    exchange `choose_exchange` picks.  Returns (slice tensors, lo, n,
+    info) where info names the exchange and its per-rank send bytes."""
+    names = _names(tensors)
+    chosen, nnz_max = choose_exchange(tensors["rows"], P, len(names), group, mode)
+    if chosen == "all_to_all":
+        out, lo, n = all_to_all_partials(tensors, P, group)
+    else:
+        out, lo, n = reduce_scatter_partials(tensors, P, group)
+    info = {"mode": chosen, "backend": dist.get_backend(group),
+            "world_size": dist.get_world_size(group), "nnz_max": nnz_max,
+            "send_bytes": exchange_bytes(P, nnz_max, len(names))[chosen]}
+    return out, lo, n, info
 
 
 def slice_bitmap(mask: torch.Tensor, lo: int, n: int) -> torch.Tensor:

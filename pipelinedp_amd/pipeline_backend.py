@@ -2,9 +2,10 @@
 
 `PipelineBackend` keeps the reference's abstract interface
 (pipeline_backend.py:38-195) so code written against it type-checks here.
-`MI355XBackend` is the only backend in this package.  Its DP hot path is
-`aggregate_device` / `select_partitions_device`, which `DPEngine` calls
-instead of building the reference's graph of generic ops; the generic ops
+`MI355XBackend` is the only backend in this package.  `DPEngine.aggregate` /
+`select_partitions` detect it and return a lazy `DeviceAggregation`
+(device_aggregate.py) instead of building the reference's graph of generic
+ops; the generic ops
 are implemented with plain Python generators (LocalBackend semantics,
 pipeline_backend.py:477-583) for user-side collection plumbing only -- the
 DP aggregation never runs through them.
@@ -212,10 +213,16 @@ class MI355XBackend(_HostCollectionOps, PipelineBackend):
         makes the noise reproducible, which is only acceptable in tests.
       process_group: torch.distributed group for multi-GPU aggregation
         (records must be sharded by privacy id); None = single GPU.
+      exchange: how the ranks merge their per-partition partials
+        (distributed.py): 'auto' (by occupancy), 'reduce_scatter' (dense)
+        or 'all_to_all' (sparse rows of the occupied partitions).
     """
 
     def __init__(self, device: Optional[int] = None, seed: Optional[int] = None,
-                 process_group=None):
+                 process_group=None, exchange: str = "auto"):
+        if exchange not in ("auto", "reduce_scatter", "all_to_all"):
+            raise ValueError(f"unknown exchange {exchange!r}")
+        self.exchange = exchange
         if device is None:
             device = int(os.environ.get("LOCAL_RANK", 0))
         self.device_index = device

@@ -327,6 +327,51 @@ def gen_sampling_distribution(trials=4000):
                        partitions=[10, 11, 12], histogram=hist), f, indent=1)
 
 
+def gen_sampling_distribution_modes(trials=4000):
+    """The same outcome histograms for the two other bounders on the same
+    rows (public partitions 10, 11, 12), seeded like the cross + per one:
+
+    * PER_PRIVACY_ID (contribution_bounders.py:108-150): max_contributions=2
+      keeps 2 of pid 1's 6 records and 2 of pid 2's 4, uniformly; outcome =
+      per-partition (count, sum) of COUNT + SUM;
+    * CROSS_PARTITION (:153-195): SUM with min/max_sum_per_partition keeps
+      mpc=2 of pid 1's 3 partitions with ALL their values, then clips each
+      pair's sum to [0, 6]; outcome = per-partition (sum, privacy_id_count).
+    """
+    rows = [(1, 10, 1.0), (1, 10, 1.0), (1, 10, 5.0), (1, 11, 2.0),
+            (1, 11, 7.0), (1, 12, 4.0), (2, 10, 3.0), (2, 10, 4.0),
+            (2, 10, 4.0), (2, 10, 9.0)]
+    modes = {
+        "per_privacy_id": (dict(metrics=[M.COUNT, M.SUM], max_contributions=2,
+                                min_value=0.0, max_value=10.0),
+                           ("count", "sum")),
+        "cross_partition": (dict(metrics=[M.SUM, M.PRIVACY_ID_COUNT],
+                                 max_partitions_contributed=2,
+                                 max_contributions_per_partition=1,
+                                 min_sum_per_partition=0.0, max_sum_per_partition=6.0),
+                            ("sum", "privacy_id_count")),
+    }
+    ex = pipeline_dp.DataExtractors(privacy_id_extractor=lambda r: r[0],
+                                    partition_extractor=lambda r: r[1],
+                                    value_extractor=lambda r: r[2])
+    for name, (kw, fields) in modes.items():
+        hist = {}
+        for t in range(trials):
+            np.random.seed(t)
+            acc = pipeline_dp.NaiveBudgetAccountant(1.0, 1e-6)
+            eng = pipeline_dp.DPEngine(acc, pipeline_dp.LocalBackend())
+            res = eng.aggregate(rows, pipeline_dp.AggregateParams(**kw), ex,
+                                public_partitions=[10, 11, 12])
+            acc.compute_budgets()
+            out = dict((k, tuple(float(getattr(m, f)) for f in fields)) for k, m in res)
+            key = json.dumps([out[10], out[11], out[12]])
+            hist[key] = hist.get(key, 0) + 1
+        with open(os.path.join(HERE, f"sampling_distribution_{name}.json"), "w") as f:
+            json.dump(dict(rows=rows, trials=trials, params=_params_to_json(kw),
+                           fields=list(fields), partitions=[10, 11, 12], histogram=hist),
+                      f, indent=1)
+
+
 def gen_select_partitions():
     """select_partitions with a keep-all strategy: the set of partitions."""
     pid, pk, _ = synthetic(9, 3000, 200, 150, 0, 1)
@@ -349,6 +394,7 @@ def main():
         json.dump(metas, f, indent=1)
     gen_budget_splits()
     gen_sampling_distribution()
+    gen_sampling_distribution_modes()
     gen_select_partitions()
     print("wrote", len(metas), "aggregate cases")
 

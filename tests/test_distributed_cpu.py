@@ -33,7 +33,7 @@ FIELDS = dict(mode=0, sum_mode=1, metric_mask=7, max_partitions_contributed=3,
               n_partitions=P)
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, mode):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     pid, pk, val = _data()
@@ -43,7 +43,11 @@ def _worker(rank, world, port, q):
     part = oracle.bound_aggregate(pid[m], pk[m], val[m], FIELDS, 99, rec_ids=np.nonzero(m)[0])
     tens = {k: torch.as_tensor(part[k]) for k in ("rows", "count", "sum")}
     tens.update(nsum=None, nsq=None)
-    out, lo, n = distributed.reduce_scatter_partials(tens, P, dist.group.WORLD)
+    if mode == "reduce_scatter":
+        out, lo, n = distributed.reduce_scatter_partials(tens, P, dist.group.WORLD)
+    else:
+        out, lo, n, info = distributed.exchange_partials(tens, P, dist.group.WORLD, mode)
+        assert info["mode"] == "all_to_all" and info["world_size"] == world
     # kept results: partitions of this slice with rows > 0, values = counts
     ids = torch.nonzero(out["rows"] > 0).flatten() + lo
     vals = out["count"][ids - lo].to(torch.float64).view(-1, 1)
@@ -63,12 +67,13 @@ def _free_port():
     return p
 
 
-def test_two_rank_merge_equals_single_process():
-    world = 2
+@pytest.mark.parametrize("world,mode", [(2, "reduce_scatter"), (2, "all_to_all"),
+                                        (3, "all_to_all")])
+def test_rank_merge_equals_single_process(world, mode):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, mode)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in range(world)]
@@ -85,7 +90,44 @@ def test_two_rank_merge_equals_single_process():
         assert np.array_equal(np.sort(g_ids), want_ids)
         bits = np.unpackbits(sl, bitorder="little")[:n]
         assert np.array_equal(np.nonzero(bits)[0] + lo, np.arange(0, P, 3)[(np.arange(0, P, 3) >= lo) & (np.arange(0, P, 3) < lo + n)])
-    assert sorted(r[1] for r in res) == [0, 500]
+    chunk = (P + world - 1) // world
+    assert sorted(r[1] for r in res) == [r * chunk for r in range(world)]
+
+
+def _choose_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    Pbig = 1_000_000
+    rows = torch.zeros(Pbig, dtype=torch.int64)
+    # rank 1 is the fuller one: the choice must follow the largest occupancy
+    nnz = 1000 if rank == 0 else (50_000 if q is not None and world == 2 else 1000)
+    rows[torch.arange(nnz) * 7] = 1
+    sparse = distributed.choose_exchange(rows, Pbig, 3, dist.group.WORLD)
+    rows[:] = 1
+    dense = distributed.choose_exchange(rows, Pbig, 3, dist.group.WORLD)
+    forced = distributed.choose_exchange(rows, Pbig, 3, dist.group.WORLD, "all_to_all")
+    q.put((rank, sparse, dense, forced))
+    dist.destroy_process_group()
+
+
+def test_exchange_choice_is_global_and_by_occupancy():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_choose_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, sparse, dense, forced in res:
+        assert sparse == ("all_to_all", 50_000)   # max over ranks, same on both
+        assert dense == ("reduce_scatter", 1_000_000)
+        assert forced == ("all_to_all", 1_000_000)
+    b = distributed.exchange_bytes(100_000_000, 10_000_000, 5)
+    assert b["all_to_all"] * 6 < b["reduce_scatter"]
 
 
 def test_shard_is_deterministic_and_balanced():

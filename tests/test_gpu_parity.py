@@ -350,3 +350,42 @@ def test_gpu_candidate_prefilter_and_restart(built, mpc):
     assert np.array_equal(got["rows"], ref["rows"])
     assert np.array_equal(got["count"], ref["count"])
     assert np.allclose(got["sum"], ref["sum"], rtol=1e-9, atol=1e-9)
+
+
+@pytest.mark.parametrize("name,kw", MODES, ids=[m[0] for m in MODES])
+@pytest.mark.parametrize("kernel", ["sort", "hash"])
+def test_gpu_small_chunk_kernels_match_oracle(built, monkeypatch, name, kw, kernel):
+    """Both small-chunk bounding kernels -- the sort-based default of the
+    cross-partition modes (dpg_sortb.h) and the hash-table kernel
+    (dpg_wave.h; DPG_BOUND_HASH forces it) -- keep exactly the oracle's
+    records, with bounding triggered (mpc 3 over ~40 partitions per id,
+    mcpp 2 over hot partitions).  PER_PRIVACY_ID always takes the hash
+    kernel; the stage marker says which one ran."""
+    if kernel == "hash":
+        monkeypatch.setenv("DPG_BOUND_HASH", "1")
+    else:
+        monkeypatch.delenv("DPG_BOUND_HASH", raising=False)
+    P = 3000
+    pid, pk, val = _dataset(41, 400_000, 10_000, P, zipf=1.1)
+    params = pdp.AggregateParams(**kw)
+    backend = pdp.MI355XBackend(device=0, seed=SEED)
+    acc = pdp.NaiveBudgetAccountant(1.0, 1e-6)
+    res = pdp.DPEngine(acc, backend).aggregate(
+        pdp.ColumnarData(pid=torch.as_tensor(pid), pk=torch.as_tensor(pk),
+                         value=torch.as_tensor(val), n_partitions=P),
+        params, pdp.DataExtractors("pid", "pk", "value"), public_partitions=list(range(P)))
+    acc.compute_budgets()
+    res.noise_enabled = False
+    res.materialize()
+    ran = [k for k in backend.ctx.stage_times() if k.startswith("bound.kernel=")]
+    want = "hash" if (kernel == "hash" or name == "per_pid") else "sort"
+    assert ran == ["bound.kernel=" + want]
+    plan = res.plan
+    ref = oracle.bound_aggregate(pid, pk, val if plan.needs_values() else None,
+                                 res.last_bound_fields, SEED, public_mask=oracle.bitmap(range(P), P))
+    got = {k: (v.cpu().numpy() if v is not None else None) for k, v in res.last_partials.items()}
+    assert np.array_equal(got["rows"], ref["rows"])
+    assert np.array_equal(got["count"], ref["count"])
+    for k in ("sum", "nsum", "nsq"):
+        if got[k] is not None:
+            assert np.allclose(got[k], ref[k], rtol=1e-9, atol=1e-9), k
