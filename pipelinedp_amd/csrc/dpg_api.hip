@@ -425,6 +425,7 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
         return fail(ctx, DPG_ERR_KEY_RANGE,
                     "privacy id outside its declared range or partition key outside [0, P)");
     uint4 *chunk_list = chunks;
+    size_t chunk_cap = B;  // entries of chunk_list
     const uint4 *mchunk_list = mchunks;
     const R *refined = recs;
     // global-memory leftovers: (buffer, starts, counts, level-1 buckets, number)
@@ -479,6 +480,7 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
             HIP_TRY(hipMemcpyAsync(&hctl, ctl, sizeof(Control), hipMemcpyDeviceToHost, s));
             HIP_TRY(hipStreamSynchronize(s));
             chunk_list = chunks2;
+            chunk_cap = (size_t)hctl.n_chunks + B2;
             mchunk_list = mchunks2;
             refined = rbuf;
             g_base = rbuf;
@@ -514,8 +516,6 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     // Gm 256-thread workgroups over the medium ones (launched only if there
     // are any), the global-memory path last; workgroup g of the Gw + Gm + 1
     // writes its items to items[wg_off[g], ...)
-    // resident single-wave workgroups per CU: the LDS share or the register
-    // file, whichever binds (a static schedule must not oversubscribe)
     // one kernel per bounding family (PER_PRIVACY_ID or cross-partition), so
     // that the hot one holds one path only
     // the cross-partition modes sort (dpg_sortb.h) when the partition key
@@ -524,24 +524,32 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     auto wave_kern = per_pid ? k_bound_waves<KeyT, Item, R, true> : k_bound_waves<KeyT, Item, R, false>;
     size_t wave_lds = WL::TOTAL;
     bool use_sort = false;
-    if constexpr (!ItemTraits<Item>::preagg) {
+    if constexpr (!ItemTraits<Item>::preagg)
         use_sort = !per_pid && pl.pkbits <= kSkPkBits && std::getenv("DPG_BOUND_HASH") == nullptr;
-        if (use_sort) {
-            wave_kern = k_bound_sorted<Item, R>;
-            wave_lds = SortLayout<Item, R>::TOTAL;
-        }
+    // resident single-wave workgroups per CU of a kernel: the LDS share or
+    // the register file, whichever binds, rounded down to a multiple of the
+    // 4 SIMDs: the static schedule gives every wave the same share of
+    // chunks, so two waves sharing a SIMD next to SIMDs with one would finish
+    // last (same-box A/B, config 4 with 32-KB working sets: 5 waves per CU
+    // 42 ms, 4 per CU 29.7 ms)
+    auto waves_per_cu = [&](const void *kern, size_t lds) {
+        int wpc = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&wpc, kern, 64, lds) != hipSuccess ||
+            wpc <= 0)
+            wpc = 1;
+        int pc = std::min(wpc, (int)std::min<size_t>(16, (160 * 1024) / lds));
+        if (pc > 4) pc &= ~3;
+        if (const char *e = std::getenv("DPG_DEBUG_WPC"))  // debug: occupancy experiments
+            pc = std::max(1, std::min(pc, std::atoi(e)));
+        return pc;
+    };
+    const void *narrow = nullptr, *wide = nullptr;
+    if constexpr (!ItemTraits<Item>::preagg) {
+        narrow = (const void *)k_bound_sorted<Item, R, false>;
+        wide = (const void *)k_bound_sorted<Item, R, true>;
+        if (use_sort) wave_lds = SortLayout<Item, R>::TOTAL;
     }
-    int wpc = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&wpc, wave_kern, 64, wave_lds) != hipSuccess ||
-        wpc <= 0)
-        wpc = 1;
-    // waves per CU rounded down to a multiple of the 4 SIMDs: the static
-    // schedule gives every wave the same share of chunks, so two waves
-    // sharing a SIMD next to SIMDs with one would finish last (same-box
-    // A/B, config 4 with 32-KB working sets: 5 waves per CU 42 ms, 4 per
-    // CU 29.7 ms)
-    int per_cu = std::min(wpc, (int)std::min<size_t>(16, (160 * 1024) / wave_lds));
-    if (per_cu > 4) per_cu &= ~3;
+    const int per_cu = waves_per_cu(use_sort ? narrow : (const void *)wave_kern, wave_lds);
     const uint32_t Gw = (uint32_t)(ctx->n_cu * per_cu);
     const uint32_t Gm = hctl.n_mchunks ? (uint32_t)std::min<uint32_t>(
                                              ctx->n_cu * CL::PER_CU, hctl.n_mchunks)
@@ -574,15 +582,32 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
         HIP_TRY(hipMemsetAsync(pc, 0, 48 * 8, s));
         bpl.phase_cyc = pc;
     }
-    (void)hipFuncSetAttribute((const void *)wave_kern,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)wave_lds);
     // zero-length marker stage: which small-chunk kernel bounded this call
     stage(ctx, s, use_sort ? "bound.kernel=sort" : "bound.kernel=hash");
     stage(ctx, s, "bound");
-    wave_kern<<<Gw, 64, wave_lds, s>>>(recs, refined, hrec, chunk_list,
-                                                          &ctl->n_chunks, bpl, items, wg_off,
-                                                          wg_cnt);
-    LAUNCH_CHECK();
+    if constexpr (!ItemTraits<Item>::preagg) if (use_sort) {
+        WS(defer, uint8_t, "bound.defer", std::max<size_t>(chunk_cap, 1));
+        (void)hipFuncSetAttribute(narrow, hipFuncAttributeMaxDynamicSharedMemorySize, (int)wave_lds);
+        (void)hipFuncSetAttribute(wide, hipFuncAttributeMaxDynamicSharedMemorySize, (int)wave_lds);
+        k_bound_sorted<Item, R, false><<<Gw, 64, wave_lds, s>>>(
+            recs, refined, hrec, chunk_list, &ctl->n_chunks, bpl, items, wg_off, wg_cnt, defer, Gw);
+        LAUNCH_CHECK();
+        // chunks with more candidates than the narrow kernel sorts
+        stage(ctx, s, "bound.wide");
+        const uint32_t Gx = std::min<uint32_t>(Gw, (uint32_t)(ctx->n_cu * waves_per_cu(wide, wave_lds)));
+        BoundParams bpx = bpl;
+        bpx.phase_cyc = nullptr;
+        k_bound_sorted<Item, R, true><<<Gx, 64, wave_lds, s>>>(
+            recs, refined, hrec, chunk_list, &ctl->n_chunks, bpx, items, wg_off, wg_cnt, defer, Gw);
+        LAUNCH_CHECK();
+    }
+    if (!use_sort) {
+        (void)hipFuncSetAttribute((const void *)wave_kern,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)wave_lds);
+        wave_kern<<<Gw, 64, wave_lds, s>>>(recs, refined, hrec, chunk_list, &ctl->n_chunks, bpl,
+                                           items, wg_off, wg_cnt);
+        LAUNCH_CHECK();
+    }
     if (prog) watchdog_wait(s, prog, Gw, "k_bound_waves");
     stage(ctx, s, "bound.medium");
     if (Gm) {

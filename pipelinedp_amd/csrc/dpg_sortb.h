@@ -21,12 +21,13 @@
 //      records whose pair priority is below a bound aimed at ~CAND x (mpc +
 //      2 sqrt(mpc) + 2) records (a pair's records share its priority, so
 //      whole pairs pass or fail); candidates are compacted into LDS
-//   S  bitonic sort of the candidates' (skey, ordinal) in registers: E =
+//   S  bitonic sort of the candidates' (skey, record index) in registers: E =
 //      1, 2, 4 or 8 elements per lane (64 E >= candidates), cross-lane steps
 //      by DPP / ds_swizzle / bpermute
 //   P  pair starts, pair ordinals (wave scan), pair rank inside the pid; a
 //      filtered pid that shows fewer than mpc candidate pairs restarts the
-//      chunk with all of its records (rare); a pair is kept iff rank < mpc
+//      chunk with all of its records, re-read from HBM (rare); a pair is
+//      kept iff rank < mpc
 //   M  records of kept pairs gather their values; pairs over mcpp rank their
 //      records by record priority (contribution_bounders.py:74-76) inside
 //      the pair's segment
@@ -52,6 +53,14 @@ namespace dpg {
 constexpr uint32_t kSkPkBits = 24;  // partition-key bits of the sort key
 constexpr uint64_t kSkPad = ~0ull;  // padding elements (real keys have bit 63 clear)
 
+// The wave's LDS working set is kept under 10 KB (COUNT / SUM items) so that
+// 16 waves share a CU: the kernel is latency-bound per wave (same-box A/B,
+// config 2: 4 waves per CU 24.2 ms, 8 waves per CU 12.5 ms), so resident
+// waves are what hides the LDS round trips and the value gathers.  The sort
+// payload is the record index itself (no per-position copy of the records),
+// pair starts are 16-bit, and the candidate area is reused: candidate keys
+// and indices -> record keys of over-full pairs (phase M) -> accumulators
+// per pair (phase F).
 template <class Item, class R>
 struct SortLayout {
     static constexpr int NACC = ItemTraits<Item>::var ? (ItemTraits<Item>::sum ? 3 : 2) : 1;
@@ -60,16 +69,31 @@ struct SortLayout {
     static constexpr size_t CBND = PIDV + 4 * kWCq;    // candidate bound
     static constexpr size_t PBASE = CBND + 4 * kWCq;   // ordinal of the pid's first pair
     static constexpr size_t FULL = PBASE + 4 * kWCq;   // pid shows >= mpc candidate pairs
-    static constexpr size_t CKEY = FULL + 4 * kWCq;    // candidate keys; after the sort
-                                                       // the record keys by position
-    static constexpr size_t RECS = CKEY + 8 * kWCap;   // the chunk's records by position
-    static constexpr size_t CORD = RECS + a16(sizeof(R) * kWCap);  // candidate -> position
-    static constexpr size_t PSTART = CORD + a16(2 * kWCap);        // first position per pair
-    static constexpr size_t ACC = PSTART + a16(4 * (kWCap + 1));
-    static constexpr size_t END = ACC + 8 * kWCap * NACC;
-    static constexpr size_t TOTAL = (END + 4095) & ~(size_t)4095;
+    // first position per pair (u16); before the sort: occupied pid slots (u32)
+    static constexpr size_t PSTART = FULL + 4 * kWCq;
+    static constexpr size_t CK = PSTART + a16(2 * (kWCap + 1) > 4 * kWCq ? 2 * (kWCap + 1) : 4 * kWCq);
+    // candidate keys u64[kWCap] + record indices u32[kWCap]; then record
+    // keys by position (u64); then NACC accumulators per pair (f64)
+    static constexpr size_t CIDX = CK + 8 * kWCap;
+    static constexpr size_t CKSZ = 12 * kWCap > 8 * NACC * kWCap ? 12 * kWCap : 8 * NACC * kWCap;
+    static constexpr size_t END = CK + CKSZ;
+    static constexpr size_t TOTAL = (END + 255) & ~(size_t)255;
     static_assert(TOTAL <= 40 * 1024, "sort working set too large");
 };
+
+// Two instantiations of the kernel (kWide):
+//  * narrow: chunks of <= kNarrowCand candidates (E <= 4 elements per lane),
+//    registers for 4 waves per SIMD (<= 128 VGPRs; the bound parameters stay
+//    in scalar registers); a chunk with more candidates is only flagged
+//    (defer[w] = 1) and left to
+//  * wide: E <= 8, 2 waves per SIMD (the 8-element sort network needs ~230
+//    VGPRs), which walks the flagged chunks of the narrow kernel's
+//    workgroups and appends to their item regions.
+// Config 2 (~120 candidates per chunk) never reaches the wide kernel; chunks
+// of many small privacy ids (every record a candidate) do.
+constexpr uint32_t kNarrowCand = 256;
+constexpr int kNarrowWPS = 4;  // waves per SIMD the narrow kernel's registers allow
+constexpr int kWideWPS = 2;
 
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
 #pragma unroll
@@ -200,12 +224,11 @@ __device__ __forceinline__ bool sort_chunk(uint32_t nc, char *smem, const BoundP
     uint32_t *cbnd = reinterpret_cast<uint32_t *>(smem + L::CBND);
     uint32_t *pbase = reinterpret_cast<uint32_t *>(smem + L::PBASE);
     uint32_t *full = reinterpret_cast<uint32_t *>(smem + L::FULL);
-    uint64_t *ckey = reinterpret_cast<uint64_t *>(smem + L::CKEY);
-    uint64_t *rks = ckey;  // after the sort
-    const R *recl = reinterpret_cast<const R *>(smem + L::RECS);
-    const uint16_t *cord = reinterpret_cast<const uint16_t *>(smem + L::CORD);
-    uint32_t *pstart = reinterpret_cast<uint32_t *>(smem + L::PSTART);
-    double *acc = reinterpret_cast<double *>(smem + L::ACC);
+    uint64_t *ckey = reinterpret_cast<uint64_t *>(smem + L::CK);
+    const uint32_t *cidx = reinterpret_cast<const uint32_t *>(smem + L::CIDX);
+    uint64_t *rks = ckey;  // after the sort (phase M)
+    uint16_t *pstart = reinterpret_cast<uint16_t *>(smem + L::PSTART);
+    double *acc = reinterpret_cast<double *>(smem + L::CK);  // phase F
     double *acc_nsum = acc + (kSum ? kWCap : 0);
     double *acc_nsq = acc_nsum + kWCap;
     const uint32_t lane = __lane_id();
@@ -216,7 +239,7 @@ __device__ __forceinline__ bool sort_chunk(uint32_t nc, char *smem, const BoundP
     const bool part_clip = bp.sum_mode == DPG_SUM_CLIP_PARTITION;
     constexpr uint32_t kPkMask = (1u << kSkPkBits) - 1u;
 
-    // ---- S: sort (key, record position)
+    // ---- S: sort (key, record index)
     uint64_t k[E];
     uint32_t o[E];
 #pragma unroll
@@ -224,7 +247,7 @@ __device__ __forceinline__ bool sort_chunk(uint32_t nc, char *smem, const BoundP
         const uint32_t i = lane * E + j;
         const uint32_t ic = min(i, (uint32_t)kWCap - 1);
         const uint64_t x = ckey[ic];
-        const uint32_t y = cord[ic];
+        const uint32_t y = cidx[ic];
         k[j] = i < nc ? x : kSkPad;
         o[j] = i < nc ? y : 0u;
     }
@@ -256,10 +279,10 @@ __device__ __forceinline__ bool sort_chunk(uint32_t nc, char *smem, const BoundP
 #pragma unroll
     for (int j = 0; j < E; ++j) {
         a[j] += before;  // pair ordinal
-        if ((psm >> j) & 1u) pstart[a[j]] = lane * E + j;
+        if ((psm >> j) & 1u) pstart[a[j]] = (uint16_t)(lane * E + j);
         if ((pidm >> j) & 1u) pbase[(uint32_t)(k[j] >> 56) & (kWCq - 1)] = a[j];
     }
-    if (lane == 0) pstart[npairs] = nc;
+    if (lane == 0) pstart[npairs] = (uint16_t)nc;
     wave_sync();
     uint32_t kpm = 0;
     {
@@ -301,13 +324,13 @@ __device__ __forceinline__ bool sort_chunk(uint32_t nc, char *smem, const BoundP
 
     // ---- M: kept pairs; values of their records; mcpp sample of over-full
     // pairs by record priority
-    uint32_t st[E], len[E], idx[E];
+    uint32_t st[E], len[E];
+    const uint32_t (&idx)[E] = o;
     double v[E];
 #pragma unroll
     for (int j = 0; j < E; ++j) {
         st[j] = pstart[min(a[j], (uint32_t)kWCap - 1)];
         len[j] = pstart[min(a[j] + 1, (uint32_t)kWCap)];
-        idx[j] = RecOps<R>::idx(recl[min(o[j], (uint32_t)kWCap - 1)], f);
     }
     uint32_t overm = 0, maxlen = 0;
 #pragma unroll
@@ -353,6 +376,7 @@ __device__ __forceinline__ bool sort_chunk(uint32_t nc, char *smem, const BoundP
     // ---- F: accumulators of kept records, one item per kept pair
     const uint32_t em = psm & kpm;
     if (need_v) {
+        wave_sync();  // the accumulators overwrite the record keys of phase M
 #pragma unroll
         for (int j = 0; j < E; ++j) {
             if (!((em >> j) & 1u)) continue;
@@ -404,22 +428,22 @@ __device__ __forceinline__ bool sort_chunk(uint32_t nc, char *smem, const BoundP
     return true;
 }
 
-// One small chunk: pid counts, pid hashes and candidate bounds, candidate
-// compaction, then sort_chunk (a second round with the short pids' bounds
-// lifted when the first finds one).
-template <class Item, class R>
-__device__ __forceinline__ uint32_t sort_bound_chunk(const R (&r)[kWRPT], uint32_t n, uint32_t d1,
-                                                     uint32_t hbase, char *smem,
-                                                     const BoundParams &bp, Item *items,
-                                                     uint32_t nitems, PhaseTimer &clk,
-                                                     uint32_t hbound, uint32_t hidx) {
+// One round: (first round only) records per pid slot, pid hashes and
+// candidate bounds; pair priorities; candidates compacted into LDS; sort and
+// bound.  Returns kRoundDone, kRoundRestart (see sort_chunk) or, in the
+// narrow kernel, kRoundDefer (more than kNarrowCand candidates).
+constexpr int kRoundRestart = 0, kRoundDone = 1, kRoundDefer = 2;
+template <class Item, class R, bool kFirst, bool kWide>
+__device__ __forceinline__ int sort_round(const R (&r)[kWRPT], uint32_t n, uint32_t d1,
+                                           uint32_t hbase, char *smem, const BoundParams &bp,
+                                           Item *items, uint32_t &nitems, PhaseTimer &clk,
+                                           uint32_t hbound, uint32_t hidx) {
     using L = SortLayout<Item, R>;
     uint32_t *pidv = reinterpret_cast<uint32_t *>(smem + L::PIDV);
     uint32_t *pidc = reinterpret_cast<uint32_t *>(smem + L::PIDC);
     uint32_t *cbnd = reinterpret_cast<uint32_t *>(smem + L::CBND);
-    uint64_t *ckey = reinterpret_cast<uint64_t *>(smem + L::CKEY);
-    R *recl = reinterpret_cast<R *>(smem + L::RECS);
-    uint16_t *cord = reinterpret_cast<uint16_t *>(smem + L::CORD);
+    uint64_t *ckey = reinterpret_cast<uint64_t *>(smem + L::CK);
+    uint32_t *cidx = reinterpret_cast<uint32_t *>(smem + L::CIDX);
     uint32_t *olist = reinterpret_cast<uint32_t *>(smem + L::PSTART);
     const uint32_t lane = __lane_id();
     const Fmt f = bp.fmt;
@@ -428,8 +452,9 @@ __device__ __forceinline__ uint32_t sort_bound_chunk(const R (&r)[kWRPT], uint32
     const uint32_t hshift = f.kbits - f.b1;
     const uint32_t kn = (n + 63) >> 6;  // occupied record slots per lane (uniform)
 
-    // ---- A: records to LDS; records per pid slot
-    uint64_t sk[kWRPT];  // q << 56 | pk (pair priority added below)
+    // ---- A: records per pid slot, pair priorities, candidates
+    uint64_t sk[kWRPT];  // q << 56 | pp << 24 | pk
+    uint32_t ix[kWRPT];
     uint32_t validm = 0;
 #pragma unroll
     for (int k = 0; k < kWRPT && k < (int)kn; ++k) {
@@ -437,14 +462,14 @@ __device__ __forceinline__ uint32_t sort_bound_chunk(const R (&r)[kWRPT], uint32
         const uint64_t key = RecOps<R>::key(r[k], f);
         const uint32_t q = ((uint32_t)(key >> pkb) - hbase) & (kWCq - 1);
         sk[k] = ((uint64_t)q << 56) | (key & pkmask);
-        recl[lane + 64u * k] = r[k];
+        ix[k] = RecOps<R>::idx(r[k], f);
     }
+    if constexpr (kFirst) {
 #pragma unroll
-    for (int k = 0; k < kWRPT && k < (int)kn; ++k)
-        if ((validm >> k) & 1u) atomicAdd(&pidc[(uint32_t)(sk[k] >> 56)], 1u);
-    wave_sync();
-    // pid hash and candidate bound of the occupied slots (compacted)
-    {
+        for (int k = 0; k < kWRPT && k < (int)kn; ++k)
+            if ((validm >> k) & 1u) atomicAdd(&pidc[(uint32_t)(sk[k] >> 56)], 1u);
+        wave_sync();
+        // pid hash and candidate bound of the occupied slots (compacted)
         const float cmul = DPG_SORT_CAND_C * ((float)bp.mpc + 2.0f * sqrtf((float)bp.mpc) + 2.0f);
         uint32_t nocc = 0;
 #pragma unroll
@@ -468,144 +493,190 @@ __device__ __forceinline__ uint32_t sort_bound_chunk(const R (&r)[kWRPT], uint32
                                                                 : (uint32_t)(fr * 4294967296.0f));
             }
         }
+        wave_sync();
     }
-    wave_sync();
+    uint32_t nc = 0;
     {
-        uint32_t pv[kWRPT];
-#pragma unroll
-        for (int k = 0; k < kWRPT && k < (int)kn; ++k) pv[k] = pidv[(uint32_t)(sk[k] >> 56)];
-#pragma unroll
-        for (int k = 0; k < kWRPT && k < (int)kn; ++k)
-            sk[k] |= (uint64_t)pair_prio_h(pv[k], (uint32_t)sk[k]) << kSkPkBits;
-    }
-    mark(bp, 0, clk);
-    for (uint32_t round = 0;; ++round) {
-        // ---- candidates (pair priority within the pid's bound), compacted
-        uint32_t cb[kWRPT];
-#pragma unroll
-        for (int k = 0; k < kWRPT && k < (int)kn; ++k) cb[k] = cbnd[(uint32_t)(sk[k] >> 56)];
-        uint32_t nc = 0;
+        uint32_t pv[kWRPT], cb[kWRPT];
 #pragma unroll
         for (int k = 0; k < kWRPT && k < (int)kn; ++k) {
-            const bool c = ((validm >> k) & 1u) && (uint32_t)(sk[k] >> kSkPkBits) <= cb[k];
+            pv[k] = pidv[(uint32_t)(sk[k] >> 56)];
+            cb[k] = cbnd[(uint32_t)(sk[k] >> 56)];
+        }
+#pragma unroll
+        for (int k = 0; k < kWRPT && k < (int)kn; ++k) {
+            const uint32_t pp = pair_prio_h(pv[k], (uint32_t)sk[k]);
+            sk[k] |= (uint64_t)pp << kSkPkBits;
+            const bool c = ((validm >> k) & 1u) && pp <= cb[k];
             const uint64_t bc = __ballot(c);
             if (c) {
                 const uint32_t e = nc + lanes_below(bc);
                 ckey[e] = sk[k];
-                cord[e] = (uint16_t)(lane + 64u * k);
+                cidx[e] = ix[k];
             }
             nc += (uint32_t)__popcll(bc);
         }
-        wave_sync();
-        const bool last = round > 0;
-        bool done;
-        if (nc <= 64)
-            done = sort_chunk<Item, R, 1>(nc, smem, bp, last, hbound, hidx, items, nitems, clk);
-        else if (nc <= 128)
-            done = sort_chunk<Item, R, 2>(nc, smem, bp, last, hbound, hidx, items, nitems, clk);
-        else if (nc <= 256)
-            done = sort_chunk<Item, R, 4>(nc, smem, bp, last, hbound, hidx, items, nitems, clk);
-        else
-            done = sort_chunk<Item, R, 8>(nc, smem, bp, last, hbound, hidx, items, nitems, clk);
-        wave_sync();
-        if (done) break;
+    }
+    wave_sync();
+    mark(bp, 0, clk);
+    if constexpr (!kWide) {
+        if (nc > kNarrowCand) return kRoundDefer;
+    }
+    constexpr bool last = !kFirst;
+    bool done;
+    if (nc <= 64)
+        done = sort_chunk<Item, R, 1>(nc, smem, bp, last, hbound, hidx, items, nitems, clk);
+    else if (nc <= 128)
+        done = sort_chunk<Item, R, 2>(nc, smem, bp, last, hbound, hidx, items, nitems, clk);
+    else if (!kWide || nc <= 256)
+        done = sort_chunk<Item, R, 4>(nc, smem, bp, last, hbound, hidx, items, nitems, clk);
+    else
+        done = sort_chunk<Item, R, kWide ? 8 : 4>(nc, smem, bp, last, hbound, hidx, items, nitems,
+                                                  clk);
+    wave_sync();
+    return done ? kRoundDone : kRoundRestart;
+}
+
+// One small chunk.  When the first round finds a filtered pid short of mpc
+// candidate pairs, the chunk's records are loaded again (L2-hot) and a
+// second round runs with that pid's bound lifted: keeping the records in
+// registers across the sort would cost the occupancy the kernel lives on.
+// Returns true when the chunk was deferred to the wide kernel (nothing
+// emitted).
+template <class Item, class R, bool kWide>
+__device__ __forceinline__ bool sort_bound_chunk(const R (&r0)[kWRPT], const R *base, uint32_t n,
+                                                 uint32_t d1, uint32_t hbase, char *smem,
+                                                 const BoundParams &bp, Item *items,
+                                                 uint32_t &nitems, PhaseTimer &clk,
+                                                 uint32_t hbound, uint32_t hidx) {
+    using L = SortLayout<Item, R>;
+    uint32_t *pidc = reinterpret_cast<uint32_t *>(smem + L::PIDC);
+    const uint32_t lane = __lane_id();
+    int st = sort_round<Item, R, true, kWide>(r0, n, d1, hbase, smem, bp, items, nitems, clk,
+                                              hbound, hidx);
+    if (st == kRoundRestart) {
+        R r[kWRPT];
+#pragma unroll
+        for (int k = 0; k < kWRPT; ++k) r[k] = base[min(lane + 64u * k, n - 1)];
+        st = sort_round<Item, R, false, kWide>(r, n, d1, hbase, smem, bp, items, nitems, clk,
+                                               hbound, hidx);
     }
 #pragma unroll
     for (int j = 0; j < (int)(kWCq / 64); ++j) pidc[lane + 64u * j] = 0;
     wave_sync();
     mark(bp, 5, clk);
-    return nitems;
+    return st == kRoundDefer;
 }
 
 // Persistent single-wave workgroups walk the small-chunk list statically
-// (w, w + G, ...), as k_bound_waves; workgroup g appends its items to
-// items[wg_off[g], ...) and leaves the count in wg_cnt[g].
-template <class Item, class R>
-__global__ __launch_bounds__(64, 2) void k_bound_sorted(const R *recs, const R *refined,
-                                                        const R *heavy, const uint4 *chunks,
-                                                        const uint32_t *n_chunks, BoundParams bp,
-                                                        Item *items, const int64_t *wg_off,
-                                                        uint32_t *wg_cnt) {
+// (w, w + G1, ...), as k_bound_waves; narrow workgroup g appends its items
+// to items[wg_off[g], ...) and leaves the count in wg_cnt[g], and flags the
+// chunks it defers in defer[w].  The wide kernel's workgroup g2 then takes
+// the narrow workgroups g = g2, g2 + gridDim.x, ... and bounds their flagged
+// chunks, appending behind wg_cnt[g].  The narrow kernel loads the next
+// chunk's records while the current one is bounded.
+template <class Item, class R, bool kWide>
+__global__ __launch_bounds__(64, kWide ? kWideWPS : kNarrowWPS) void k_bound_sorted(
+    const R *recs, const R *refined, const R *heavy, const uint4 *chunks, const uint32_t *n_chunks,
+    BoundParams bp, Item *items, const int64_t *wg_off, uint32_t *wg_cnt, uint8_t *defer,
+    uint32_t G1) {
     using L = SortLayout<Item, R>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     PhaseTimer clk;
     timer_start(bp, clk);
-    // parameters used in one phase each: vector registers (see vreg; the
-    // kernel is short of scalar registers, not of vector ones)
-    bp.lo = vreg(bp.lo);
-    bp.hi = vreg(bp.hi);
-    bp.lo_pp = vreg(bp.lo_pp);
-    bp.hi_pp = vreg(bp.hi_pp);
-    bp.mid = vreg(bp.mid);
-    bp.seed = vreg(bp.seed);
-    bp.pid_min = vreg(bp.pid_min);
-    bp.rec_base = vreg(bp.rec_base);
-    bp.hash.mask = vreg(bp.hash.mask);
-    bp.hash.i1 = vreg(bp.hash.i1);
-    bp.hash.i2 = vreg(bp.hash.i2);
-    bp.mpc = vreg(bp.mpc);
-    bp.mcpp = vreg(bp.mcpp);
-    bp.fmt.ib = vreg(bp.fmt.ib);
-    bp.fmt.pkbits = vreg(bp.fmt.pkbits);
-    bp.fmt.kbits = vreg(bp.fmt.kbits);
-    bp.fmt.b1 = vreg(bp.fmt.b1);
-    bp.value = vreg(bp.value);
-    bp.heavy_fb = vreg(bp.heavy_fb);
-    bp.heavy_nfb = vreg(bp.heavy_nfb);
+    if constexpr (kWide) {
+        // parameters used in one phase each: vector registers (see vreg;
+        // the wide kernel is short of scalar registers, not of vector ones)
+        bp.lo = vreg(bp.lo);
+        bp.hi = vreg(bp.hi);
+        bp.lo_pp = vreg(bp.lo_pp);
+        bp.hi_pp = vreg(bp.hi_pp);
+        bp.mid = vreg(bp.mid);
+        bp.seed = vreg(bp.seed);
+        bp.pid_min = vreg(bp.pid_min);
+        bp.rec_base = vreg(bp.rec_base);
+        bp.hash.mask = vreg(bp.hash.mask);
+        bp.hash.i1 = vreg(bp.hash.i1);
+        bp.hash.i2 = vreg(bp.hash.i2);
+        bp.mpc = vreg(bp.mpc);
+        bp.mcpp = vreg(bp.mcpp);
+        bp.fmt.ib = vreg(bp.fmt.ib);
+        bp.fmt.pkbits = vreg(bp.fmt.pkbits);
+        bp.fmt.kbits = vreg(bp.fmt.kbits);
+        bp.fmt.b1 = vreg(bp.fmt.b1);
+        bp.value = vreg(bp.value);
+        bp.heavy_fb = vreg(bp.heavy_fb);
+        bp.heavy_nfb = vreg(bp.heavy_nfb);
+    }
     const uint32_t nch = __builtin_amdgcn_readfirstlane(*n_chunks);
-    Item *my_items = items + wg_off[blockIdx.x];
     const uint32_t lane = __lane_id();
     {
         uint32_t *pidc = reinterpret_cast<uint32_t *>(smem + L::PIDC);
         for (uint32_t i = lane; i < kWCq; i += 64) pidc[i] = 0;
     }
     wave_sync();
-    R r[kWRPT], rn[kWRPT];
-    const uint32_t G = gridDim.x;
-    uint32_t w = blockIdx.x;
-    uint32_t n = 0, d1 = 0, hb = 0, hbound = 0, hidx = 0, nitems = 0;
-    uint4 dn = make_uint4(0, 0, 0, 0);
-    if (w < nch) {
-        const uint4 d = make_uint4(__builtin_amdgcn_readfirstlane(chunks[w].x),
-                                   __builtin_amdgcn_readfirstlane(chunks[w].y),
-                                   __builtin_amdgcn_readfirstlane(chunks[w].z),
-                                   __builtin_amdgcn_readfirstlane(chunks[w].w));
-        n = d.y & kChunkCount;
-        d1 = d.z & 0xFFFFu;
-        hb = d.w;
-        hbound = heavy_bound(d);
-        hidx = d.x / (uint32_t)kWCap;
-        const R *b = wave_chunk_base(d, recs, refined, heavy);
+    auto desc = [&](uint32_t w) {
+        return make_uint4(__builtin_amdgcn_readfirstlane(chunks[w].x),
+                          __builtin_amdgcn_readfirstlane(chunks[w].y),
+                          __builtin_amdgcn_readfirstlane(chunks[w].z),
+                          __builtin_amdgcn_readfirstlane(chunks[w].w));
+    };
+    if constexpr (!kWide) {
+        uint32_t nitems = 0;
+        Item *my_items = items + wg_off[blockIdx.x];
+        R r[kWRPT], rn[kWRPT];
+        uint4 d = make_uint4(0, 0, 0, 0);
+        if (blockIdx.x < nch) {
+            d = desc(blockIdx.x);
+            const uint32_t n = d.y & kChunkCount;
+            const R *b = wave_chunk_base(d, recs, refined, heavy);
 #pragma unroll
-        for (int k = 0; k < kWRPT; ++k) r[k] = b[min(lane + 64u * k, n - 1)];
-        if (w + G < nch) dn = chunks[w + G];
-    }
-    for (; w < nch; w += G) {
-        uint4 dnn = make_uint4(0, 0, 0, 0);
-        if (w + 2 * G < nch) dnn = chunks[w + 2 * G];
-        const uint4 du = make_uint4(__builtin_amdgcn_readfirstlane(dn.x),
-                                    __builtin_amdgcn_readfirstlane(dn.y),
-                                    __builtin_amdgcn_readfirstlane(dn.z),
-                                    __builtin_amdgcn_readfirstlane(dn.w));
-        const uint32_t nn = du.y & kChunkCount;
-        // the next chunk's records load while this one is processed
-        if (nn > 0) {
-            const R *nb = wave_chunk_base(du, recs, refined, heavy);
-#pragma unroll
-            for (int k = 0; k < kWRPT; ++k) rn[k] = nb[min(lane + 64u * k, nn - 1)];
+            for (int k = 0; k < kWRPT; ++k) r[k] = b[min(lane + 64u * k, n - 1)];
         }
-        nitems = sort_bound_chunk<Item, R>(r, n, d1, hb, smem, bp, my_items, nitems, clk, hbound,
-                                           hidx);
+        for (uint32_t w = blockIdx.x; w < nch; w += G1) {
+            uint4 du = make_uint4(0, 0, 0, 0);
+            if (w + G1 < nch) {
+                du = desc(w + G1);
+                const uint32_t nn = du.y & kChunkCount;
+                const R *nb = wave_chunk_base(du, recs, refined, heavy);
 #pragma unroll
-        for (int k = 0; k < kWRPT; ++k) r[k] = rn[k];
-        n = nn;
-        d1 = du.z & 0xFFFFu;
-        hb = du.w;
-        hbound = heavy_bound(du);
-        hidx = du.x / (uint32_t)kWCap;
-        dn = dnn;
+                for (int k = 0; k < kWRPT; ++k) rn[k] = nb[min(lane + 64u * k, nn - 1)];
+            }
+            const bool df = sort_bound_chunk<Item, R, false>(
+                r, wave_chunk_base(d, recs, refined, heavy), d.y & kChunkCount, d.z & 0xFFFFu, d.w,
+                smem, bp, my_items, nitems, clk, heavy_bound(d), d.x / (uint32_t)kWCap);
+            if (lane == 0) defer[w] = df ? 1 : 0;
+#pragma unroll
+            for (int k = 0; k < kWRPT; ++k) r[k] = rn[k];
+            d = du;
+        }
+        if (lane == 0) wg_cnt[blockIdx.x] = nitems;
+    } else {
+        for (uint32_t g = blockIdx.x; g < G1; g += gridDim.x) {
+            uint32_t nitems = __builtin_amdgcn_readfirstlane(wg_cnt[g]);
+            Item *my_items = items + wg_off[g];
+            bool any = false;
+            // the flags of 64 of g's chunks per load, then the set ones
+            for (uint32_t i0 = 0; g + i0 * G1 < nch; i0 += 64) {
+                const uint32_t wl = g + (i0 + lane) * G1;
+                for (uint64_t fm = __ballot(wl < nch && defer[min(wl, nch - 1)] != 0); fm;
+                     fm &= fm - 1) {
+                    const uint32_t w = g + (i0 + (uint32_t)__builtin_ctzll(fm)) * G1;
+                    any = true;
+                    const uint4 d = desc(w);
+                    const uint32_t n = d.y & kChunkCount;
+                    const R *b = wave_chunk_base(d, recs, refined, heavy);
+                    R r[kWRPT];
+#pragma unroll
+                    for (int k = 0; k < kWRPT; ++k) r[k] = b[min(lane + 64u * k, n - 1)];
+                    sort_bound_chunk<Item, R, true>(r, b, n, d.z & 0xFFFFu, d.w, smem, bp, my_items,
+                                                    nitems, clk, heavy_bound(d),
+                                                    d.x / (uint32_t)kWCap);
+                }
+            }
+            if (any && lane == 0) wg_cnt[g] = nitems;
+        }
     }
-    if (lane == 0) wg_cnt[blockIdx.x] = nitems;
     timer_flush(bp, clk);
 }
 
