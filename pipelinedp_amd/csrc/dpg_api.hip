@@ -366,6 +366,11 @@ BoundParams to_bound(const dpg_bound_params *p, uint64_t seed) {
     b.mid = p->min_value + (p->max_value - p->min_value) / 2;
     b.seed = seed;
     b.rec_base = p->rec_id_offset;
+    // candidate records per filtered pid in the sort kernel: DPG_SORT_CAND_C
+    // x (mpc + 2 sqrt(mpc) + 2); DPG_SORT_CAND_C overrides it for experiments
+    float cc = kSortCandC;
+    if (const char *e = std::getenv("DPG_SORT_CAND_C")) cc = (float)std::atof(e);
+    b.cand_mul = cc * ((float)b.mpc + 2.0f * std::sqrt((float)b.mpc) + 2.0f);
     return b;
 }
 
@@ -525,7 +530,11 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     size_t wave_lds = WL::TOTAL;
     bool use_sort = false;
     if constexpr (!ItemTraits<Item>::preagg)
-        use_sort = !per_pid && pl.pkbits <= kSkPkBits && std::getenv("DPG_BOUND_HASH") == nullptr;
+        use_sort = !per_pid && std::getenv("DPG_BOUND_HASH") == nullptr &&
+                   (pl.pkbits <= kSkPkBits || (sizeof(R) == 12 && pl.pkbits <= 32));
+    // partition keys wider than the sort key's 24 bits: the wide-key kernels
+    // (their low bits ride in the sort payload; 12-byte records only)
+    const bool wpk = pl.pkbits > kSkPkBits;
     // resident single-wave workgroups per CU of a kernel: the LDS share or
     // the register file, whichever binds, rounded down to a multiple of the
     // 4 SIMDs: the static schedule gives every wave the same share of
@@ -545,9 +554,18 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     };
     const void *narrow = nullptr, *wide = nullptr;
     if constexpr (!ItemTraits<Item>::preagg) {
-        narrow = (const void *)k_bound_sorted<Item, R, false>;
-        wide = (const void *)k_bound_sorted<Item, R, true>;
-        if (use_sort) wave_lds = SortLayout<Item, R>::TOTAL;
+        if (use_sort && !wpk) {
+            narrow = (const void *)k_bound_sorted<Item, R, false, false>;
+            wide = (const void *)k_bound_sorted<Item, R, true, false>;
+            wave_lds = SortLayout<Item, R, false>::TOTAL;
+        }
+        if constexpr (sizeof(R) == 12) {
+            if (use_sort && wpk) {
+                narrow = (const void *)k_bound_sorted<Item, R, false, true>;
+                wide = (const void *)k_bound_sorted<Item, R, true, true>;
+                wave_lds = SortLayout<Item, R, true>::TOTAL;
+            }
+        }
     }
     const int per_cu = waves_per_cu(use_sort ? narrow : (const void *)wave_kern, wave_lds);
     const uint32_t Gw = (uint32_t)(ctx->n_cu * per_cu);
@@ -589,16 +607,26 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
         WS(defer, uint8_t, "bound.defer", std::max<size_t>(chunk_cap, 1));
         (void)hipFuncSetAttribute(narrow, hipFuncAttributeMaxDynamicSharedMemorySize, (int)wave_lds);
         (void)hipFuncSetAttribute(wide, hipFuncAttributeMaxDynamicSharedMemorySize, (int)wave_lds);
-        k_bound_sorted<Item, R, false><<<Gw, 64, wave_lds, s>>>(
-            recs, refined, hrec, chunk_list, &ctl->n_chunks, bpl, items, wg_off, wg_cnt, defer, Gw);
-        LAUNCH_CHECK();
-        // chunks with more candidates than the narrow kernel sorts
-        stage(ctx, s, "bound.wide");
-        const uint32_t Gx = std::min<uint32_t>(Gw, (uint32_t)(ctx->n_cu * waves_per_cu(wide, wave_lds)));
-        BoundParams bpx = bpl;
-        bpx.phase_cyc = nullptr;
-        k_bound_sorted<Item, R, true><<<Gx, 64, wave_lds, s>>>(
-            recs, refined, hrec, chunk_list, &ctl->n_chunks, bpx, items, wg_off, wg_cnt, defer, Gw);
+        auto launch = [&](auto wpk_tag) {
+            constexpr bool W = decltype(wpk_tag)::value;
+            k_bound_sorted<Item, R, false, W><<<Gw, 64, wave_lds, s>>>(
+                recs, refined, hrec, chunk_list, &ctl->n_chunks, bpl, items, wg_off, wg_cnt, defer,
+                Gw);
+            // chunks with more candidates than the narrow kernel sorts
+            stage(ctx, s, "bound.wide");
+            const uint32_t Gx = std::min<uint32_t>(
+                Gw, (uint32_t)(ctx->n_cu * waves_per_cu(wide, wave_lds)));
+            BoundParams bpx = bpl;
+            bpx.phase_cyc = nullptr;
+            k_bound_sorted<Item, R, true, W><<<Gx, 64, wave_lds, s>>>(
+                recs, refined, hrec, chunk_list, &ctl->n_chunks, bpx, items, wg_off, wg_cnt, defer,
+                Gw);
+        };
+        if (!wpk) {
+            launch(std::false_type{});
+        } else if constexpr (sizeof(R) == 12) {
+            launch(std::true_type{});
+        }
         LAUNCH_CHECK();
     }
     if (!use_sort) {

@@ -47,6 +47,7 @@ struct BoundParams {
     unsigned long long *phase_cyc;  // debug: shader cycles per phase (or null)
     uint32_t *heavy_fb;    // heavy buckets handed back to k_bound_big (indices)
     uint32_t *heavy_nfb;   // their number
+    float cand_mul;        // sort kernel: candidate records aimed at per filtered pid
 };
 
 // privacy id of a bucket's pid-hash residual

@@ -44,11 +44,10 @@
 namespace dpg {
 
 // candidate bound of the sort kernel (records per pid aimed at, times
-// mpc + 2 sqrt(mpc) + 2); the sort makes extra candidates cheap, restarts
-// (a pid short of mpc candidate pairs) cost a second sort
-#ifndef DPG_SORT_CAND_C
-#define DPG_SORT_CAND_C 2.0f
-#endif
+// mpc + 2 sqrt(mpc) + 2: BoundParams::cand_mul); restarts (a pid short of
+// mpc candidate pairs) cost a second round, candidates past 64 / 128 / 256
+// per chunk a sort twice as wide
+constexpr float kSortCandC = 1.5f;  // same-box A/B, config 2 bound: 2.0 9.03 ms, 1.5 7.49, 1.25 7.47 + more restarts
 
 constexpr uint32_t kSkPkBits = 24;  // partition-key bits of the sort key
 constexpr uint64_t kSkPad = ~0ull;  // padding elements (real keys have bit 63 clear)
@@ -61,7 +60,7 @@ constexpr uint64_t kSkPad = ~0ull;  // padding elements (real keys have bit 63 c
 // pair starts are 16-bit, and the candidate area is reused: candidate keys
 // and indices -> record keys of over-full pairs (phase M) -> accumulators
 // per pair (phase F).
-template <class Item, class R>
+template <class Item, class R, bool kWPk = false>
 struct SortLayout {
     static constexpr int NACC = ItemTraits<Item>::var ? (ItemTraits<Item>::sum ? 3 : 2) : 1;
     static constexpr size_t PIDC = 0;                  // records per pid slot
@@ -76,7 +75,10 @@ struct SortLayout {
     // keys by position (u64); then NACC accumulators per pair (f64)
     static constexpr size_t CIDX = CK + 8 * kWCap;
     static constexpr size_t CKSZ = 12 * kWCap > 8 * NACC * kWCap ? 12 * kWCap : 8 * NACC * kWCap;
-    static constexpr size_t END = CK + CKSZ;
+    // wide partition keys (kWPk): the low pk bits the sort key has no room
+    // for, per candidate (u8)
+    static constexpr size_t CPKL = CK + CKSZ;
+    static constexpr size_t END = CPKL + (kWPk ? kWCap : 0);
     static constexpr size_t TOTAL = (END + 255) & ~(size_t)255;
     static_assert(TOTAL <= 40 * 1024, "sort working set too large");
 };
@@ -94,6 +96,9 @@ struct SortLayout {
 constexpr uint32_t kNarrowCand = 256;
 constexpr int kNarrowWPS = 4;  // waves per SIMD the narrow kernel's registers allow
 constexpr int kWideWPS = 2;
+#ifndef DPG_SORT_VREG
+#define DPG_SORT_VREG 1  // bound parameters the narrow kernel keeps in VGPRs (0, 1 or 2 groups)
+#endif
 
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
 #pragma unroll
@@ -140,7 +145,7 @@ __device__ __forceinline__ uint64_t xlane64(uint64_t x, int m) {
 // a lane's E elements need no exchange; the others read the partner lane's
 // element through xlane.  The only lane-dependent decision is "is this the
 // lower index", one lane bit.  Equal keys never move, so partners agree.
-template <int E>
+template <int E, bool kLex = false>
 __device__ __forceinline__ void bitonic_sort(uint64_t (&k)[E], uint32_t (&o)[E]) {
     constexpr int LOG_S = E == 1 ? 6 : E == 2 ? 7 : E == 4 ? 8 : 9;
     constexpr int LOG_E = LOG_S - 6;
@@ -148,8 +153,12 @@ __device__ __forceinline__ void bitonic_sort(uint64_t (&k)[E], uint32_t (&o)[E])
     // of the chunk loop (they would live in scalar registers all along)
     uint32_t lid = __lane_id();
     asm volatile("" : "+v"(lid));
+    // kLex: (key, payload) lexicographically (every element distinct)
+    auto less = [](uint64_t a, uint32_t oa, uint64_t b, uint32_t ob) {
+        return kLex ? (a < b || (a == b && oa < ob)) : a < b;
+    };
     auto cex = [&](int j, int j2) {  // in-lane compare-exchange, min to j
-        const bool sw = k[j] > k[j2];
+        const bool sw = less(k[j2], o[j2], k[j], o[j]);
         const uint64_t a = k[j], b = k[j2];
         const uint32_t oa = o[j], ob = o[j2];
         k[j] = sw ? b : a;
@@ -179,7 +188,7 @@ __device__ __forceinline__ void bitonic_sort(uint64_t (&k)[E], uint32_t (&o)[E])
             }
 #pragma unroll
             for (int j = 0; j < E; ++j) {
-                const bool take = lower ? (y[j] < k[j]) : (y[j] > k[j]);
+                const bool take = lower ? less(y[j], yo[j], k[j], o[j]) : less(k[j], o[j], y[j], yo[j]);
                 k[j] = take ? y[j] : k[j];
                 o[j] = take ? yo[j] : o[j];
             }
@@ -199,7 +208,7 @@ __device__ __forceinline__ void bitonic_sort(uint64_t (&k)[E], uint32_t (&o)[E])
                 for (int j = 0; j < E; ++j) {
                     const uint64_t y = xlane64(k[j], m);
                     const uint32_t yo = xlane(o[j], m);
-                    const bool take = lower ? (y < k[j]) : (y > k[j]);
+                    const bool take = lower ? less(y, yo, k[j], o[j]) : less(k[j], o[j], y, yo);
                     k[j] = take ? y : k[j];
                     o[j] = take ? yo : o[j];
                 }
@@ -209,16 +218,27 @@ __device__ __forceinline__ void bitonic_sort(uint64_t (&k)[E], uint32_t (&o)[E])
 }
 
 // Sorts the nc candidates and bounds them (phases S, P, M, F of the header).
-// Returns false when the chunk must restart: the filtered pids short of mpc
-// candidate pairs have had their bound lifted (their CBND set to all-pass).
-// Per-element flags live in per-lane bit masks (bit j = element j).
-template <class Item, class R, int E>
-__device__ __forceinline__ bool sort_chunk(uint32_t nc, char *smem, const BoundParams &bp,
+// Returns kRoundRestart when the chunk must restart: the filtered pids short
+// of mpc candidate pairs have had their bound lifted (their CBND set to
+// all-pass).  Per-element flags live in per-lane bit masks (bit j = element
+// j).
+//
+// kWPk (partition keys of 25..32 bits): the sort key carries the top 24 pk
+// bits, the payload the candidate's position e (9 bits) and the low pk bits
+// (idx is read back from CIDX by e).  Pairs then differ in (key, low bits);
+// two pairs of one pid with equal key (same priority, same top bits; ~2^-56
+// per pair of pairs) may interleave under a key-only comparator, so the
+// narrow kernel defers such a chunk (kRoundDefer) to the wide kernel, whose
+// comparator (kLex) orders by (key, payload).
+constexpr int kRoundRestart = 0, kRoundDone = 1, kRoundDefer = 2;
+template <class Item, class R, int E, bool kWPk, bool kLex>
+__device__ __forceinline__ int sort_chunk(uint32_t nc, char *smem, const BoundParams &bp,
                                            bool last_round, uint32_t hbound, uint32_t hidx,
                                            Item *items, uint32_t &nitems, PhaseTimer &clk) {
-    using L = SortLayout<Item, R>;
+    using L = SortLayout<Item, R, kWPk>;
     constexpr bool kVar = ItemTraits<Item>::var;
     constexpr bool kSum = ItemTraits<Item>::sum;
+    const uint8_t *cpkl = reinterpret_cast<const uint8_t *>(smem + L::CPKL);
     uint32_t *pidv = reinterpret_cast<uint32_t *>(smem + L::PIDV);
     uint32_t *pidc = reinterpret_cast<uint32_t *>(smem + L::PIDC);
     uint32_t *cbnd = reinterpret_cast<uint32_t *>(smem + L::CBND);
@@ -238,8 +258,9 @@ __device__ __forceinline__ bool sort_chunk(uint32_t nc, char *smem, const BoundP
     const bool sample = cap_pp && need_v;
     const bool part_clip = bp.sum_mode == DPG_SUM_CLIP_PARTITION;
     constexpr uint32_t kPkMask = (1u << kSkPkBits) - 1u;
+    const uint32_t pksh = kWPk ? f.pkbits - kSkPkBits : 0u;  // low pk bits in the payload
 
-    // ---- S: sort (key, record index)
+    // ---- S: sort (key, record index | kWPk: position e | low pk bits << 9)
     uint64_t k[E];
     uint32_t o[E];
 #pragma unroll
@@ -247,32 +268,39 @@ __device__ __forceinline__ bool sort_chunk(uint32_t nc, char *smem, const BoundP
         const uint32_t i = lane * E + j;
         const uint32_t ic = min(i, (uint32_t)kWCap - 1);
         const uint64_t x = ckey[ic];
-        const uint32_t y = cidx[ic];
+        const uint32_t y = kWPk ? (ic | ((uint32_t)cpkl[ic] << 9)) : cidx[ic];
         k[j] = i < nc ? x : kSkPad;
         o[j] = i < nc ? y : 0u;
     }
     full[lane] = 0;
     full[lane + 64u] = 0;
-    bitonic_sort<E>(k, o);
+    bitonic_sort<E, kLex>(k, o);
     mark(bp, 1, clk);
 
     // ---- P: pair starts, ordinals, rank inside the pid
     const uint64_t prev_last = (uint64_t)__shfl_up((long long)k[E - 1], 1, 64);
+    const uint32_t prev_o = kWPk ? (uint32_t)__shfl_up((int)o[E - 1], 1, 64) : 0u;
     uint32_t validm = 0, psm = 0, pidm = 0;
     uint32_t a[E];
     uint32_t cnt = 0;
+    bool coll = false;  // kWPk: two pairs with one key (see above)
 #pragma unroll
     for (int j = 0; j < E; ++j) {
         const uint32_t i = lane * E + j;
         const uint64_t pv = j ? k[j - 1] : prev_last;
         const bool val = i < nc;
-        const bool p = val && (i == 0 || k[j] != pv);
+        const bool lodiff = kWPk && ((o[j] >> 9) != ((j ? o[j - 1] : prev_o) >> 9));
+        const bool p = val && (i == 0 || k[j] != pv || lodiff);
+        coll |= val && i > 0 && k[j] == pv && lodiff;
         const bool d = val && (i == 0 || (k[j] >> 56) != (pv >> 56));
         validm |= val ? 1u << j : 0u;
         psm |= p ? 1u << j : 0u;
         pidm |= d ? 1u << j : 0u;
         cnt += p ? 1u : 0u;
         a[j] = cnt;  // inclusive within the lane
+    }
+    if constexpr (kWPk && !kLex) {
+        if (__ballot(coll)) return kRoundDefer;
     }
     uint32_t npairs;
     const uint32_t before = wave_excl_scan(cnt, npairs) - 1u;
@@ -315,22 +343,23 @@ __device__ __forceinline__ bool sort_chunk(uint32_t nc, char *smem, const BoundP
                 // a heavy chunk holds only its pid's candidates: the bucket
                 // goes back to the global-memory kernel (rare)
                 if (lane == 0) bp.heavy_fb[atomicAdd(bp.heavy_nfb, 1u)] = hidx;
-                return true;
+                return kRoundDone;
             }
-            return false;
+            return kRoundRestart;
         }
     }
     mark(bp, 2, clk);
 
     // ---- M: kept pairs; values of their records; mcpp sample of over-full
     // pairs by record priority
-    uint32_t st[E], len[E];
-    const uint32_t (&idx)[E] = o;
+    uint32_t st[E], len[E], idx[E], pkf[E];  // pkf: the full partition key
     double v[E];
 #pragma unroll
     for (int j = 0; j < E; ++j) {
         st[j] = pstart[min(a[j], (uint32_t)kWCap - 1)];
         len[j] = pstart[min(a[j] + 1, (uint32_t)kWCap)];
+        idx[j] = kWPk ? cidx[o[j] & (kWCap - 1)] : o[j];
+        pkf[j] = kWPk ? ((((uint32_t)k[j] & kPkMask) << pksh) | (o[j] >> 9)) : ((uint32_t)k[j] & kPkMask);
     }
     uint32_t overm = 0, maxlen = 0;
 #pragma unroll
@@ -351,8 +380,7 @@ __device__ __forceinline__ bool sort_chunk(uint32_t nc, char *smem, const BoundP
         for (int j = 0; j < E; ++j) {
             if (!((overm >> j) & 1u)) continue;
             const uint32_t q = (uint32_t)(k[j] >> 56) & (kWCq - 1);
-            rks[lane * E + j] = rec_prio_h(pidv[q], (uint32_t)k[j] & kPkMask,
-                                           (uint64_t)(bp.rec_base + idx[j]));
+            rks[lane * E + j] = rec_prio_h(pidv[q], pkf[j], (uint64_t)(bp.rec_base + idx[j]));
         }
         wave_sync();
 #pragma unroll
@@ -410,7 +438,7 @@ __device__ __forceinline__ bool sort_chunk(uint32_t nc, char *smem, const BoundP
         const uint64_t be = __ballot(e);
         if (e) {
             Item it;
-            it.pk = (uint32_t)k[j] & kPkMask;
+            it.pk = pkf[j];
             it.cnt = cap_pp ? min(len[j], bp.mcpp) : len[j];
             if constexpr (kSum) {
                 const double s = need_v ? acc[a[j]] : 0.0;
@@ -425,25 +453,26 @@ __device__ __forceinline__ bool sort_chunk(uint32_t nc, char *smem, const BoundP
         nitems += (uint32_t)__popcll(be);
     }
     mark(bp, 4, clk);
-    return true;
+    return kRoundDone;
 }
 
 // One round: (first round only) records per pid slot, pid hashes and
 // candidate bounds; pair priorities; candidates compacted into LDS; sort and
 // bound.  Returns kRoundDone, kRoundRestart (see sort_chunk) or, in the
-// narrow kernel, kRoundDefer (more than kNarrowCand candidates).
-constexpr int kRoundRestart = 0, kRoundDone = 1, kRoundDefer = 2;
-template <class Item, class R, bool kFirst, bool kWide>
+// narrow kernel, kRoundDefer (more than kNarrowCand candidates, or a key
+// collision of wide partition keys).
+template <class Item, class R, bool kFirst, bool kWide, bool kWPk>
 __device__ __forceinline__ int sort_round(const R (&r)[kWRPT], uint32_t n, uint32_t d1,
                                            uint32_t hbase, char *smem, const BoundParams &bp,
                                            Item *items, uint32_t &nitems, PhaseTimer &clk,
                                            uint32_t hbound, uint32_t hidx) {
-    using L = SortLayout<Item, R>;
+    using L = SortLayout<Item, R, kWPk>;
     uint32_t *pidv = reinterpret_cast<uint32_t *>(smem + L::PIDV);
     uint32_t *pidc = reinterpret_cast<uint32_t *>(smem + L::PIDC);
     uint32_t *cbnd = reinterpret_cast<uint32_t *>(smem + L::CBND);
     uint64_t *ckey = reinterpret_cast<uint64_t *>(smem + L::CK);
     uint32_t *cidx = reinterpret_cast<uint32_t *>(smem + L::CIDX);
+    uint8_t *cpkl = reinterpret_cast<uint8_t *>(smem + L::CPKL);
     uint32_t *olist = reinterpret_cast<uint32_t *>(smem + L::PSTART);
     const uint32_t lane = __lane_id();
     const Fmt f = bp.fmt;
@@ -451,9 +480,10 @@ __device__ __forceinline__ int sort_round(const R (&r)[kWRPT], uint32_t n, uint3
     const uint64_t pkmask = (1ull << pkb) - 1ull;
     const uint32_t hshift = f.kbits - f.b1;
     const uint32_t kn = (n + 63) >> 6;  // occupied record slots per lane (uniform)
+    const uint32_t pksh = kWPk ? pkb - kSkPkBits : 0u;
 
     // ---- A: records per pid slot, pair priorities, candidates
-    uint64_t sk[kWRPT];  // q << 56 | pp << 24 | pk
+    uint64_t sk[kWRPT];  // q << 56 | pk (pp << 24 | pk >> pksh below)
     uint32_t ix[kWRPT];
     uint32_t validm = 0;
 #pragma unroll
@@ -470,7 +500,7 @@ __device__ __forceinline__ int sort_round(const R (&r)[kWRPT], uint32_t n, uint3
             if ((validm >> k) & 1u) atomicAdd(&pidc[(uint32_t)(sk[k] >> 56)], 1u);
         wave_sync();
         // pid hash and candidate bound of the occupied slots (compacted)
-        const float cmul = DPG_SORT_CAND_C * ((float)bp.mpc + 2.0f * sqrtf((float)bp.mpc) + 2.0f);
+        const float cmul = bp.cand_mul;
         uint32_t nocc = 0;
 #pragma unroll
         for (int j = 0; j < (int)(kWCq / 64); ++j) {
@@ -505,7 +535,9 @@ __device__ __forceinline__ int sort_round(const R (&r)[kWRPT], uint32_t n, uint3
         }
 #pragma unroll
         for (int k = 0; k < kWRPT && k < (int)kn; ++k) {
-            const uint32_t pp = pair_prio_h(pv[k], (uint32_t)sk[k]);
+            const uint32_t pk = (uint32_t)sk[k];
+            const uint32_t pp = pair_prio_h(pv[k], pk);
+            if constexpr (kWPk) sk[k] = (sk[k] & ~(uint64_t)0xFFFFFFFFu) | (pk >> pksh);
             sk[k] |= (uint64_t)pp << kSkPkBits;
             const bool c = ((validm >> k) & 1u) && pp <= cb[k];
             const uint64_t bc = __ballot(c);
@@ -513,6 +545,7 @@ __device__ __forceinline__ int sort_round(const R (&r)[kWRPT], uint32_t n, uint3
                 const uint32_t e = nc + lanes_below(bc);
                 ckey[e] = sk[k];
                 cidx[e] = ix[k];
+                if constexpr (kWPk) cpkl[e] = (uint8_t)(pk & ((1u << pksh) - 1u));
             }
             nc += (uint32_t)__popcll(bc);
         }
@@ -523,18 +556,19 @@ __device__ __forceinline__ int sort_round(const R (&r)[kWRPT], uint32_t n, uint3
         if (nc > kNarrowCand) return kRoundDefer;
     }
     constexpr bool last = !kFirst;
-    bool done;
+    constexpr bool kLex = kWide && kWPk;
+    int st;
     if (nc <= 64)
-        done = sort_chunk<Item, R, 1>(nc, smem, bp, last, hbound, hidx, items, nitems, clk);
+        st = sort_chunk<Item, R, 1, kWPk, kLex>(nc, smem, bp, last, hbound, hidx, items, nitems, clk);
     else if (nc <= 128)
-        done = sort_chunk<Item, R, 2>(nc, smem, bp, last, hbound, hidx, items, nitems, clk);
+        st = sort_chunk<Item, R, 2, kWPk, kLex>(nc, smem, bp, last, hbound, hidx, items, nitems, clk);
     else if (!kWide || nc <= 256)
-        done = sort_chunk<Item, R, 4>(nc, smem, bp, last, hbound, hidx, items, nitems, clk);
+        st = sort_chunk<Item, R, 4, kWPk, kLex>(nc, smem, bp, last, hbound, hidx, items, nitems, clk);
     else
-        done = sort_chunk<Item, R, kWide ? 8 : 4>(nc, smem, bp, last, hbound, hidx, items, nitems,
-                                                  clk);
+        st = sort_chunk<Item, R, kWide ? 8 : 4, kWPk, kLex>(nc, smem, bp, last, hbound, hidx, items,
+                                                            nitems, clk);
     wave_sync();
-    return done ? kRoundDone : kRoundRestart;
+    return st;
 }
 
 // One small chunk.  When the first round finds a filtered pid short of mpc
@@ -543,22 +577,22 @@ __device__ __forceinline__ int sort_round(const R (&r)[kWRPT], uint32_t n, uint3
 // registers across the sort would cost the occupancy the kernel lives on.
 // Returns true when the chunk was deferred to the wide kernel (nothing
 // emitted).
-template <class Item, class R, bool kWide>
+template <class Item, class R, bool kWide, bool kWPk>
 __device__ __forceinline__ bool sort_bound_chunk(const R (&r0)[kWRPT], const R *base, uint32_t n,
                                                  uint32_t d1, uint32_t hbase, char *smem,
                                                  const BoundParams &bp, Item *items,
                                                  uint32_t &nitems, PhaseTimer &clk,
                                                  uint32_t hbound, uint32_t hidx) {
-    using L = SortLayout<Item, R>;
+    using L = SortLayout<Item, R, kWPk>;
     uint32_t *pidc = reinterpret_cast<uint32_t *>(smem + L::PIDC);
     const uint32_t lane = __lane_id();
-    int st = sort_round<Item, R, true, kWide>(r0, n, d1, hbase, smem, bp, items, nitems, clk,
+    int st = sort_round<Item, R, true, kWide, kWPk>(r0, n, d1, hbase, smem, bp, items, nitems, clk,
                                               hbound, hidx);
     if (st == kRoundRestart) {
         R r[kWRPT];
 #pragma unroll
         for (int k = 0; k < kWRPT; ++k) r[k] = base[min(lane + 64u * k, n - 1)];
-        st = sort_round<Item, R, false, kWide>(r, n, d1, hbase, smem, bp, items, nitems, clk,
+        st = sort_round<Item, R, false, kWide, kWPk>(r, n, d1, hbase, smem, bp, items, nitems, clk,
                                                hbound, hidx);
     }
 #pragma unroll
@@ -575,18 +609,21 @@ __device__ __forceinline__ bool sort_bound_chunk(const R (&r0)[kWRPT], const R *
 // the narrow workgroups g = g2, g2 + gridDim.x, ... and bounds their flagged
 // chunks, appending behind wg_cnt[g].  The narrow kernel loads the next
 // chunk's records while the current one is bounded.
-template <class Item, class R, bool kWide>
+template <class Item, class R, bool kWide, bool kWPk>
 __global__ __launch_bounds__(64, kWide ? kWideWPS : kNarrowWPS) void k_bound_sorted(
     const R *recs, const R *refined, const R *heavy, const uint4 *chunks, const uint32_t *n_chunks,
     BoundParams bp, Item *items, const int64_t *wg_off, uint32_t *wg_cnt, uint8_t *defer,
     uint32_t G1) {
-    using L = SortLayout<Item, R>;
+    using L = SortLayout<Item, R, kWPk>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     PhaseTimer clk;
     timer_start(bp, clk);
-    if constexpr (kWide) {
-        // parameters used in one phase each: vector registers (see vreg;
-        // the wide kernel is short of scalar registers, not of vector ones)
+    // parameters used in one phase each: vector registers (see vreg).  The
+    // wide kernel is short of scalar registers, not of vector ones: all of
+    // them; the narrow one (<= 128 VGPRs) moves the 64-bit ones only, and
+    // only with 8-byte records (the 12-byte ones need those registers)
+    constexpr int kVreg = sizeof(R) == 8 ? DPG_SORT_VREG : 0;
+    if constexpr (kWide || kVreg >= 1) {
         bp.lo = vreg(bp.lo);
         bp.hi = vreg(bp.hi);
         bp.lo_pp = vreg(bp.lo_pp);
@@ -595,6 +632,9 @@ __global__ __launch_bounds__(64, kWide ? kWideWPS : kNarrowWPS) void k_bound_sor
         bp.seed = vreg(bp.seed);
         bp.pid_min = vreg(bp.pid_min);
         bp.rec_base = vreg(bp.rec_base);
+        bp.value = vreg(bp.value);
+    }
+    if constexpr (kWide || kVreg >= 2) {
         bp.hash.mask = vreg(bp.hash.mask);
         bp.hash.i1 = vreg(bp.hash.i1);
         bp.hash.i2 = vreg(bp.hash.i2);
@@ -604,7 +644,6 @@ __global__ __launch_bounds__(64, kWide ? kWideWPS : kNarrowWPS) void k_bound_sor
         bp.fmt.pkbits = vreg(bp.fmt.pkbits);
         bp.fmt.kbits = vreg(bp.fmt.kbits);
         bp.fmt.b1 = vreg(bp.fmt.b1);
-        bp.value = vreg(bp.value);
         bp.heavy_fb = vreg(bp.heavy_fb);
         bp.heavy_nfb = vreg(bp.heavy_nfb);
     }
@@ -642,7 +681,7 @@ __global__ __launch_bounds__(64, kWide ? kWideWPS : kNarrowWPS) void k_bound_sor
 #pragma unroll
                 for (int k = 0; k < kWRPT; ++k) rn[k] = nb[min(lane + 64u * k, nn - 1)];
             }
-            const bool df = sort_bound_chunk<Item, R, false>(
+            const bool df = sort_bound_chunk<Item, R, false, kWPk>(
                 r, wave_chunk_base(d, recs, refined, heavy), d.y & kChunkCount, d.z & 0xFFFFu, d.w,
                 smem, bp, my_items, nitems, clk, heavy_bound(d), d.x / (uint32_t)kWCap);
             if (lane == 0) defer[w] = df ? 1 : 0;
@@ -669,7 +708,7 @@ __global__ __launch_bounds__(64, kWide ? kWideWPS : kNarrowWPS) void k_bound_sor
                     R r[kWRPT];
 #pragma unroll
                     for (int k = 0; k < kWRPT; ++k) r[k] = b[min(lane + 64u * k, n - 1)];
-                    sort_bound_chunk<Item, R, true>(r, b, n, d.z & 0xFFFFu, d.w, smem, bp, my_items,
+                    sort_bound_chunk<Item, R, true, kWPk>(r, b, n, d.z & 0xFFFFu, d.w, smem, bp, my_items,
                                                     nitems, clk, heavy_bound(d),
                                                     d.x / (uint32_t)kWCap);
                 }
