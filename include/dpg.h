@@ -376,7 +376,8 @@ int dpg_reduce_scatter_partials(dpg_ctx *ctx, const dpg_partials *full, dpg_part
  * names (comma separated, <= names_len bytes): e.g. "begin",
  * "partition1:hist", "partition1:scatter", "partition2:hist",
  * "partition2:scatter", "chunks", "bound.kernel=sort" (zero-length marker
- * of the small-chunk kernel that ran), "bound", "bound.medium", "bound.tail",
+ * of the small-chunk kernel that ran), "bound", "bound.wide" (sort kernel:
+ * chunks of more than 256 candidates), "bound.medium", "bound.tail",
  * "items:hist", "items:scatter", "reduce". */
 int dpg_last_stage_times(dpg_ctx *ctx, char *names, size_t names_len,
                          double *ms, int32_t max_stages, int32_t *n_stages);

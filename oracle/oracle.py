@@ -10,7 +10,8 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB = os.path.join(_HERE, "_build", "libdporacle.so")
+# DPO_LIB_PATH: an instrumented build of the same source (tests/test_asan_host.py)
+_LIB = os.environ.get("DPO_LIB_PATH") or os.path.join(_HERE, "_build", "libdporacle.so")
 
 
 class _Bound(ctypes.Structure):

@@ -255,12 +255,15 @@ template <class Src, class Rec, int IPT, int FMAX>
 int run_level(dpg_ctx *ctx, hipStream_t s, const Src &src, uint32_t S, const int64_t *seg_start,
               const uint32_t *seg_cnt, const int64_t *seg_cnt64, int64_t n_upper, uint32_t F,
               uint32_t bits, Rec *out, const char *tag, int64_t **base_out, uint32_t **tot_out,
-              uint32_t *ntiles_dev, const int64_t *out_start = nullptr, bool xcd_local = false) {
+              uint32_t *ntiles_dev, const int64_t *out_start = nullptr, bool xcd_local = false,
+              int subs = 1) {
     int st = DPG_OK;
     if (F > (uint32_t)FMAX) return fail(ctx, DPG_ERR_HIP, "internal: digit fan-out too large");
     const int64_t sub = (int64_t)kScatThreads * IPT;
-    // XCD-local mode: one sub-tile per tile, tiles of a segment on one XCD
-    const int64_t tile = xcd_local ? sub
+    // XCD-local mode: `subs` sub-tiles per tile, tiles of a segment on one
+    // XCD (every tile carries a digit histogram: tiny tiles cost histogram
+    // traffic and scan time)
+    const int64_t tile = xcd_local ? sub * std::max(1, subs)
                                    : std::max<int64_t>(sub, ((n_upper / 3072 + sub - 1) / sub) * sub);
     const uint32_t max_tiles = (uint32_t)(n_upper / tile + S + 1);
     XcdQueues xq{};
@@ -847,10 +850,25 @@ int pipeline(dpg_ctx *ctx, hipStream_t s, const int64_t *pid, const int64_t *pk,
 #ifndef DPG_L1_XCD
 #define DPG_L1_XCD 0
 #endif
+#ifndef DPG_L1_SUBS
+#define DPG_L1_SUBS 1
+#endif
+#ifndef DPG_L2_SUBS
+#define DPG_L2_SUBS 1
+#endif
+    // debug knobs for same-box experiments: XCD-local level 1, sub-tiles per
+    // XCD-local tile
+    auto env_int = [](const char *name, int dflt) {
+        const char *e = std::getenv(name);
+        return e ? std::atoi(e) : dflt;
+    };
+    const bool l1_xcd = env_int("DPG_L1_XCD", DPG_L1_XCD) != 0;
+    const int l1_subs = env_int("DPG_L1_SUBS", DPG_L1_SUBS);
+    const int l2_subs = env_int("DPG_L2_SUBS", DPG_L2_SUBS);
     int r = run_level<SrcSoAKey<R>, R, Ipt<R>::L1, 2048>(ctx, s, s1, 1u, nullptr, nullptr,
                                                          &ctl->n_scalar, n, F1, pl.b1, recA,
                                                          "partition1", &bstart, &bcnt, &ctl->ntiles[0],
-                                                         nullptr, DPG_L1_XCD != 0);
+                                                         nullptr, l1_xcd, l1_subs);
     if (r) return r;
     const R *cur = recA;
     uint32_t B = F1;
@@ -871,11 +889,11 @@ int pipeline(dpg_ctx *ctx, hipStream_t s, const int64_t *pid, const int64_t *pk,
                 ? run_level<SrcAoS<R>, R, Ipt<R>::LW, 4096>(ctx, s, s2, F1, bstart, bcnt, nullptr, n,
                                                              F2, pl.b2, recB, "partition2", &bstart,
                                                              &bcnt, &ctl->ntiles[1], nullptr,
-                                                             DPG_L2_XCD != 0)
+                                                             DPG_L2_XCD != 0, l2_subs)
                 : run_level<SrcAoS<R>, R, Ipt<R>::LN, 2048>(ctx, s, s2, F1, bstart, bcnt, nullptr, n,
                                                              F2, pl.b2, recB, "partition2", &bstart,
                                                              &bcnt, &ctl->ntiles[1], nullptr,
-                                                             DPG_L2_XCD != 0);
+                                                             DPG_L2_XCD != 0, l2_subs);
         if (r) return r;
         cur = recB;
         B = F1 * F2;
