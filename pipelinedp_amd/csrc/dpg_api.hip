@@ -250,16 +250,97 @@ __global__ void k_pid_minmax(const int64_t *pid, int64_t n, unsigned long long *
     }
 }
 
+// One partition level in grouped XCD-local mode: digit histograms per group
+// (level 1: G consecutive sub-tiles of the input, G = the CUs of one XCD;
+// later levels: one group per segment), every group's sub-tiles scattered
+// by the workgroups of one XCD at the same time (their adjacent runs meet in
+// that XCD's L2), each sub-tile reserving its runs inside the group by one
+// atomic add per digit.  No per-sub-tile histograms: at level 1 the
+// per-tile histograms of the plain XCD-local mode cost 667 MB of traffic and
+// scans per 1e9 records.  Order inside a digit is arrival order (nothing
+// downstream depends on it, DESIGN.md "Randomness").
+template <class Src, class Rec, int IPT, int FMAX>
+int run_level_grouped(dpg_ctx *ctx, hipStream_t s, const Src &src, uint32_t S,
+                      const int64_t *seg_start, const uint32_t *seg_cnt, const int64_t *seg_cnt64,
+                      int64_t n_upper, uint32_t F, uint32_t bits, Rec *out, const char *tag,
+                      int64_t **base_out, uint32_t **tot_out, uint32_t *ntiles_dev,
+                      const int64_t *out_start) {
+    int st = DPG_OK;
+    const int64_t sub = (int64_t)kScatThreads * IPT;
+    const bool single = S == 1 && !seg_start && !seg_cnt;  // level 1: all n records
+#ifndef DPG_L1_GROUP
+#define DPG_L1_GROUP 1
+#endif
+    const int64_t gsz = single ? sub * std::max<int64_t>(1, DPG_L1_GROUP * ctx->n_cu / 8)
+                               : ((int64_t)1 << 40);  // one group per segment
+    const uint32_t max_groups = (uint32_t)(n_upper / std::min<int64_t>(gsz, n_upper + 1) + S + 1);
+    const uint32_t max_subs = (uint32_t)(n_upper / sub + max_groups + 1);
+    std::string t(tag);
+    WS(groups, TileDesc, (t + ".groups").c_str(), max_groups);
+    WS(stb, uint32_t, (t + ".stb").c_str(), S);
+    WS(snt, uint32_t, (t + ".snt").c_str(), S);
+    WS(hist, uint32_t, (t + ".hist").c_str(), (size_t)max_groups * F);
+    WS(tot, uint32_t, (t + ".tot").c_str(), (size_t)S * F);
+    WS(base, int64_t, (t + ".base").c_str(), (size_t)S * F);
+    WS(tiles, TileDesc, (t + ".tiles").c_str(), max_subs);
+    WS(ngrp, uint32_t, (t + ".ngroups").c_str(), 1);
+    WS(xqq, uint32_t, (t + ".xq").c_str(), (size_t)8 * max_subs);
+    WS(xqn, uint32_t, (t + ".xqn").c_str(), 16);
+    HIP_TRY(hipMemsetAsync(xqn, 0, 16 * 4, s));
+    HIP_TRY(hipMemsetAsync(ngrp, 0, 4, s));
+    HIP_TRY(hipMemsetAsync(ntiles_dev, 0, 4, s));
+    const XcdQueues xq{xqq, xqn, xqn + 8, max_subs};
+    stage(ctx, s, (t + ":hist").c_str());
+    if (single) {
+        const uint32_t ng = (uint32_t)((n_upper + gsz - 1) / gsz);
+        k_build_tiles_single<<<(ng + 255) / 256, 256, 0, s>>>(n_upper, gsz, 1u, groups, stb, snt,
+                                                             ngrp, XcdQueues{});
+    } else {
+        k_build_tiles<<<(S + 255) / 256, 256, 0, s>>>(seg_start, seg_cnt, seg_cnt64, S, gsz,
+                                                      groups, stb, snt, ngrp, XcdQueues{});
+    }
+    LAUNCH_CHECK();
+    k_build_subtiles<<<(max_groups + 255) / 256, 256, 0, s>>>(groups, ngrp, sub, tiles, ntiles_dev,
+                                                             xq);
+    LAUNCH_CHECK();
+    if (F > 2048)
+        (void)hipFuncSetAttribute((const void *)k_hist<Src>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)(4 * F * sizeof(uint32_t)));
+    k_hist<Src><<<max_groups, kPartThreads, 4 * F * sizeof(uint32_t), s>>>(src, groups, ngrp, F, hist);
+    LAUNCH_CHECK();
+    // hist[g][d] <- the group's exclusive digit offset inside its segment
+    k_scan_tiles<<<dim3(S, (F + 63) / 64, 1), 1024, 0, s>>>(stb, snt, F, hist, tot);
+    LAUNCH_CHECK();
+    k_digit_base<<<S, 1024, 0, s>>>(out_start ? out_start : seg_start, F, tot, base);
+    LAUNCH_CHECK();
+    constexpr size_t lds = scatter_lds<Src, Rec, IPT, FMAX>();
+    static_assert(lds <= 160 * 1024, "scatter LDS");
+    auto kern = bits > 4 ? k_scatter<Src, Rec, IPT, FMAX, false> : k_scatter<Src, Rec, IPT, FMAX, true>;
+    (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    stage(ctx, s, (t + ":scatter").c_str());
+    const uint32_t gs = std::min<uint32_t>(max_subs, (uint32_t)ctx->n_cu);  // one per CU
+    kern<<<gs, kScatThreads, lds, s>>>(src, tiles, ntiles_dev, F, bits, nullptr, base, out, xq,
+                                       nullptr, nullptr, nullptr, 1u, hist);
+    LAUNCH_CHECK();
+    *base_out = base;
+    *tot_out = tot;
+    return DPG_OK;
+}
+
 // One partition level over `S` segments of the source.
 template <class Src, class Rec, int IPT, int FMAX>
 int run_level(dpg_ctx *ctx, hipStream_t s, const Src &src, uint32_t S, const int64_t *seg_start,
               const uint32_t *seg_cnt, const int64_t *seg_cnt64, int64_t n_upper, uint32_t F,
               uint32_t bits, Rec *out, const char *tag, int64_t **base_out, uint32_t **tot_out,
               uint32_t *ntiles_dev, const int64_t *out_start = nullptr, bool xcd_local = false,
-              int subs = 1) {
+              int subs = 1, bool grouped = false) {
     int st = DPG_OK;
     if (F > (uint32_t)FMAX) return fail(ctx, DPG_ERR_HIP, "internal: digit fan-out too large");
     const int64_t sub = (int64_t)kScatThreads * IPT;
+    if (grouped) return run_level_grouped<Src, Rec, IPT, FMAX>(ctx, s, src, S, seg_start, seg_cnt,
+                                                               seg_cnt64, n_upper, F, bits, out, tag,
+                                                               base_out, tot_out, ntiles_dev, out_start);
     // XCD-local mode: `subs` sub-tiles per tile, tiles of a segment on one
     // XCD (every tile carries a digit histogram: tiny tiles cost histogram
     // traffic and scan time)
@@ -330,7 +411,7 @@ int run_level(dpg_ctx *ctx, hipStream_t s, const Src &src, uint32_t S, const int
                                    : max_tiles;
     if (xcd_local) gs = std::min<uint32_t>(max_tiles, (uint32_t)ctx->n_cu);  // one per CU
     kern<<<gs, kScatThreads, lds, s>>>(src, tiles, ntiles_dev, F, bits, hist, base, out, xq,
-                                       C > 1 ? ctot : nullptr, stb, snt, C);
+                                       C > 1 ? ctot : nullptr, stb, snt, C, nullptr);
     LAUNCH_CHECK();
     *base_out = base;
     *tot_out = tot;
@@ -865,10 +946,21 @@ int pipeline(dpg_ctx *ctx, hipStream_t s, const int64_t *pid, const int64_t *pk,
     const bool l1_xcd = env_int("DPG_L1_XCD", DPG_L1_XCD) != 0;
     const int l1_subs = env_int("DPG_L1_SUBS", DPG_L1_SUBS);
     const int l2_subs = env_int("DPG_L2_SUBS", DPG_L2_SUBS);
+// grouped XCD-local levels (run_level_grouped; same-box A/B, config 2:
+// level-1 hist + scatter 1.60 + 9.35 -> 1.43 + 7.8 ms, level-2 hist 2.03 ->
+// 1.69 ms, level-2 scatter unchanged)
+#ifndef DPG_L1_GRP
+#define DPG_L1_GRP 1
+#endif
+#ifndef DPG_L2_GRP
+#define DPG_L2_GRP 1
+#endif
+    const bool l1_grp = env_int("DPG_L1_GRP", DPG_L1_GRP) != 0;
+    const bool l2_grp = env_int("DPG_L2_GRP", DPG_L2_GRP) != 0;
     int r = run_level<SrcSoAKey<R>, R, Ipt<R>::L1, 2048>(ctx, s, s1, 1u, nullptr, nullptr,
                                                          &ctl->n_scalar, n, F1, pl.b1, recA,
                                                          "partition1", &bstart, &bcnt, &ctl->ntiles[0],
-                                                         nullptr, l1_xcd, l1_subs);
+                                                         nullptr, l1_xcd, l1_subs, l1_grp);
     if (r) return r;
     const R *cur = recA;
     uint32_t B = F1;
@@ -889,11 +981,11 @@ int pipeline(dpg_ctx *ctx, hipStream_t s, const int64_t *pid, const int64_t *pk,
                 ? run_level<SrcAoS<R>, R, Ipt<R>::LW, 4096>(ctx, s, s2, F1, bstart, bcnt, nullptr, n,
                                                              F2, pl.b2, recB, "partition2", &bstart,
                                                              &bcnt, &ctl->ntiles[1], nullptr,
-                                                             DPG_L2_XCD != 0, l2_subs)
+                                                             DPG_L2_XCD != 0, l2_subs, l2_grp)
                 : run_level<SrcAoS<R>, R, Ipt<R>::LN, 2048>(ctx, s, s2, F1, bstart, bcnt, nullptr, n,
                                                              F2, pl.b2, recB, "partition2", &bstart,
                                                              &bcnt, &ctl->ntiles[1], nullptr,
-                                                             DPG_L2_XCD != 0, l2_subs);
+                                                             DPG_L2_XCD != 0, l2_subs, l2_grp);
         if (r) return r;
         cur = recB;
         B = F1 * F2;

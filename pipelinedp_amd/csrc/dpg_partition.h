@@ -288,9 +288,34 @@ __global__ void k_build_tiles_single(int64_t n, int64_t tile, uint32_t G, TileDe
     d.seg = 0;
     d.pad = 0;
     tiles[t] = d;
+    if (!xq.q) return;
     const uint32_t g = t / G, x = g & 7u;
     xq.q[(size_t)x * xq.stride + (g >> 3) * G + t % G] = t;
     atomicAdd(&xq.n[x], 1u);
+}
+
+// Grouped mode: the work items of the scatter are the sub-tiles of the
+// histogram tiles ("groups"): one thread per group appends its sub-tiles
+// (pad = group id) and queues them, in order, to XCD group % 8.
+__global__ void k_build_subtiles(const TileDesc *groups, const uint32_t *ngroups, int64_t sub,
+                                 TileDesc *tiles, uint32_t *ntiles_total, XcdQueues xq) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= *ngroups) return;
+    const TileDesc gd = groups[g];
+    const uint32_t nt = (uint32_t)((gd.end - gd.begin + sub - 1) / sub);
+    if (!nt) return;
+    const uint32_t b = atomicAdd(ntiles_total, nt);
+    for (uint32_t j = 0; j < nt; ++j) {
+        TileDesc d;
+        d.begin = gd.begin + (int64_t)j * sub;
+        d.end = min(gd.begin + (int64_t)(j + 1) * sub, gd.end);
+        d.seg = gd.seg;
+        d.pad = g;
+        tiles[b + j] = d;
+    }
+    const uint32_t x = g & 7u;
+    const uint32_t qb = atomicAdd(&xq.n[x], nt);
+    for (uint32_t j = 0; j < nt; ++j) xq.q[(size_t)x * xq.stride + qb + j] = b + j;
 }
 
 __global__ void k_build_tiles(const int64_t *seg_start, const uint32_t *seg_cnt,
@@ -535,13 +560,15 @@ __device__ __forceinline__ uint32_t block_scan_digits_t(const uint32_t *cnt, uin
 
 // Scatter's per-sub-tile digit scan: dstart[0, F] <- exclusive prefix of
 // cnt (dstart[F] = total), and for every digit cur[d] += cnt[d], cnt[d] = 0
-// (the write-out then addresses cur[d] - dstart[d + 1] + k).  Two barriers:
-// the wave totals' buffer is next written one sub-tile later, behind the
-// caller's own barriers.
+// (the write-out then addresses cur[d] - dstart[d + 1] + k).  Grouped mode
+// (goff: the group's digit offsets): the sub-tile reserves its run of every
+// digit it holds inside its group by one atomic add, cur[d] += reserved
+// start + cnt[d].  Two barriers: the wave totals' buffer is next written one
+// sub-tile later, behind the caller's own barriers.
 template <int T, int DPT>
 __device__ __forceinline__ uint32_t scatter_scan_update(uint32_t *cnt, uint32_t *dstart,
                                                         uint32_t *cur, uint32_t F,
-                                                        uint32_t *sh16) {
+                                                        uint32_t *sh16, uint32_t *goff = nullptr) {
     constexpr int NW = T / 64;
     const uint32_t d0 = DPT * threadIdx.x;
     uint32_t c[DPT], x = 0;
@@ -566,7 +593,11 @@ __device__ __forceinline__ uint32_t scatter_scan_update(uint32_t *cnt, uint32_t 
     for (int u = 0; u < DPT; ++u) {
         if (d0 + u < F) {
             dstart[d0 + u] = e;
-            cur[d0 + u] += c[u];
+            if (goff) {
+                if (c[u]) cur[d0 + u] += atomicAdd(&goff[d0 + u], c[u]) + c[u];
+            } else {
+                cur[d0 + u] += c[u];
+            }
             cnt[d0 + u] = 0;
         }
         e += c[u];
@@ -669,7 +700,7 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
                                                           const uint32_t *cbase = nullptr,
                                                           const uint32_t *seg_tile_base = nullptr,
                                                           const uint32_t *seg_ntiles = nullptr,
-                                                          uint32_t C = 1) {
+                                                          uint32_t C = 1, uint32_t *goff = nullptr) {
     constexpr int SUB = kScatThreads * IPT;
     constexpr bool kSD = !Src::kDigitFromRec;
     constexpr bool kP = HasFetchPairs<Src>::value && IPT % 2 == 0;
@@ -719,8 +750,12 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
         const uint32_t nta = seg_ntiles[td.seg], per = (nta + C - 1) / C;
         cb = cbase + ((size_t)td.seg * C + (t - seg_tile_base[td.seg]) / per) * F;
     }
+    // grouped mode: the work item is one sub-tile of group td.pad, whose runs
+    // are reserved at the digit scan
+    uint32_t *gof = goff ? goff + (size_t)td.pad * F : nullptr;
     for (uint32_t d = tid; d < F; d += kScatThreads) {
-        cur[d] = (uint32_t)(base[(size_t)td.seg * F + d] + off[(size_t)t * F + d] + (cb ? cb[d] : 0u));
+        cur[d] = (uint32_t)(base[(size_t)td.seg * F + d] +
+                            (goff ? 0u : off[(size_t)t * F + d] + (cb ? cb[d] : 0u)));
         cnt[d] = 0;
     }
     // software pipeline: the raw loads of sub-tile j + 1 are issued right
@@ -793,7 +828,7 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
         }
         __syncthreads();
         const uint32_t total =
-            scatter_scan_update<kScatThreads, FMAX / kScatThreads>(cnt, dstart, cur, F, sh16);
+            scatter_scan_update<kScatThreads, FMAX / kScatThreads>(cnt, dstart, cur, F, sh16, gof);
         {
             uint32_t ds[IPT];
 #pragma unroll
