@@ -45,6 +45,20 @@ struct HasFetchPairs<Src, decltype((void)Src::kFetchPairs)> {
     static constexpr bool value = Src::kFetchPairs;
 };
 
+// Sources whose fetch is a plain indexed load may prefetch across tiles (the
+// XCD-local scatter's next tile; SrcSeg's fetch holds a per-lane search).
+#ifndef DPG_XTILE_PF
+#define DPG_XTILE_PF 1
+#endif
+template <class Src, class = void>
+struct HasTilePrefetch {
+    static constexpr bool value = false;
+};
+template <class Src>
+struct HasTilePrefetch<Src, decltype((void)Src::kTilePrefetch)> {
+    static constexpr bool value = Src::kTilePrefetch && DPG_XTILE_PF;
+};
+
 // Sources without a pair view (kPairs false) take the one-record loop.
 template <class Src, class = void>
 struct HasPairs {
@@ -61,6 +75,23 @@ struct TileDesc {
     uint32_t pad;
 };
 
+// A tile descriptor read by a uniform index, kept in scalar registers (the
+// loops over its sub-tiles hold barriers: their trip counts must be
+// visibly wave-uniform).
+__device__ __forceinline__ TileDesc uniform_tile(const TileDesc *tiles, uint32_t t) {
+    const TileDesc d = tiles[t];
+    auto u64 = [](int64_t x) {
+        return (int64_t)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)x >> 32)) << 32) |
+                         (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)x));
+    };
+    TileDesc r;
+    r.begin = u64(d.begin);
+    r.end = u64(d.end);
+    r.seg = __builtin_amdgcn_readfirstlane(d.seg);
+    r.pad = __builtin_amdgcn_readfirstlane(d.pad);
+    return r;
+}
+
 // ---------------------------------------------------------------- sources
 // Level 1: the caller's int64 pid / pk columns -> R (key residual, index).
 // Drops records of non-public partitions.  Keys outside the declared ranges
@@ -69,6 +100,7 @@ struct TileDesc {
 template <class R>
 struct SrcSoAKey {
     static constexpr bool kDigitFromRec = false;
+    static constexpr bool kTilePrefetch = true;
     // the scatter loads only the low word of the privacy id: the digit and
     // the stored key depend on (pid - pid_min) mod 2^32 alone, and the
     // histogram pass, which reads the whole column, raises the range error
@@ -154,6 +186,7 @@ struct SrcSoAKey {
 template <class R>
 struct SrcAoS {
     static constexpr bool kDigitFromRec = true;
+    static constexpr bool kTilePrefetch = true;
     using Raw = R;
     const R *a;
     Fmt f;
@@ -728,39 +761,13 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
     __shared__ uint32_t sh_next;
     const uint32_t xq_id = blockIdx.x & 7u;
     const uint32_t xq_len = xq.q ? xq.n[xq_id] : 0u;
-    for (uint32_t it = blockIdx.x;; it += gridDim.x) {
-    uint32_t t;
-    if (xq.q) {
-        __syncthreads();  // every thread has read the previous sh_next
-        if (tid == 0) sh_next = atomicAdd(&xq.next[xq_id], 1u);
-        __syncthreads();
-        const uint32_t w = __builtin_amdgcn_readfirstlane(sh_next);
-        if (w >= xq_len) break;
-        t = __builtin_amdgcn_readfirstlane(xq.q[(size_t)xq_id * xq.stride + w]);
-    } else {
-        if (it >= nt) break;
-        t = it;
-    }
-    const TileDesc td = tiles[t];
+    constexpr uint32_t kNone = 0xFFFFFFFFu;
     Src src = src_in;  // per-thread copy (sources may cache lookup state)
-    __syncthreads();   // the previous tile's write-out has read cur / dstart
-    // chunked tile scan: the tile's offset is relative to its chunk
-    const uint32_t *cb = nullptr;
-    if (cbase) {
-        const uint32_t nta = seg_ntiles[td.seg], per = (nta + C - 1) / C;
-        cb = cbase + ((size_t)td.seg * C + (t - seg_tile_base[td.seg]) / per) * F;
-    }
-    // grouped mode: the work item is one sub-tile of group td.pad, whose runs
-    // are reserved at the digit scan
-    uint32_t *gof = goff ? goff + (size_t)td.pad * F : nullptr;
-    for (uint32_t d = tid; d < F; d += kScatThreads) {
-        cur[d] = (uint32_t)(base[(size_t)td.seg * F + d] +
-                            (goff ? 0u : off[(size_t)t * F + d] + (cb ? cb[d] : 0u)));
-        cnt[d] = 0;
-    }
-    // software pipeline: the raw loads of sub-tile j + 1 are issued right
-    // after sub-tile j is staged in LDS, so they are in flight during j's
-    // write-out
+    // software pipeline: the raw loads of the next sub-tile -- of this tile,
+    // or the first one of the next tile -- are issued right after the
+    // current sub-tile is staged in LDS, so they are in flight during its
+    // write-out.  (Grouped XCD-local levels have one sub-tile per tile: the
+    // next tile's id is dequeued at the start of the current one.)
     // Loads are unconditional with the index clamped into the sub-tile (a
     // guarded load becomes a branch with its own vmcnt(0) wait, serialising
     // the sub-tile's loads); lanes past the end re-read the last record.
@@ -790,8 +797,44 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
 #pragma unroll
         for (int j = 0; j < IPT; ++j) raw[j] = src.fetch(b0 + min(elem(j), lim - 1));
     };
+    // the first tile (tiles are never empty: the tile builders cut
+    // ceil(n / tile) tiles of n > 0 records)
+    uint32_t it = blockIdx.x;  // static schedule: it, it + gridDim.x, ...
+    uint32_t t = kNone;
+    if (xq.q) {
+        if (tid == 0) sh_next = atomicAdd(&xq.next[xq_id], 1u);
+        __syncthreads();
+        const uint32_t w = __builtin_amdgcn_readfirstlane(sh_next);
+        if (w < xq_len) t = __builtin_amdgcn_readfirstlane(xq.q[(size_t)xq_id * xq.stride + w]);
+    } else if (it < nt) {
+        t = it;
+    }
+    if (t == kNone) return;
+    TileDesc td = uniform_tile(tiles, t);
     load_sub(td.begin, (uint32_t)min<int64_t>(SUB, td.end - td.begin));
+    for (;;) {
+    // the next tile's queue slot: one atomic by thread 0, issued now,
+    // published in LDS with the first ranking barrier below
+    uint32_t nq = 0;
+    if (xq.q && tid == 0) nq = atomicAdd(&xq.next[xq_id], 1u);
+    __syncthreads();   // the previous tile's write-out has read cur / dstart / sh_next
+    // chunked tile scan: the tile's offset is relative to its chunk
+    const uint32_t *cb = nullptr;
+    if (cbase) {
+        const uint32_t nta = seg_ntiles[td.seg], per = (nta + C - 1) / C;
+        cb = cbase + ((size_t)td.seg * C + (t - seg_tile_base[td.seg]) / per) * F;
+    }
+    // grouped mode: the work item is one sub-tile of group td.pad, whose runs
+    // are reserved at the digit scan
+    uint32_t *gof = goff ? goff + (size_t)td.pad * F : nullptr;
+    for (uint32_t d = tid; d < F; d += kScatThreads) {
+        cur[d] = (uint32_t)(base[(size_t)td.seg * F + d] +
+                            (goff ? 0u : off[(size_t)t * F + d] + (cb ? cb[d] : 0u)));
+        cnt[d] = 0;
+    }
     __syncthreads();
+    uint32_t tn = kNone;
+    TileDesc tdn = td;
     for (int64_t sb = td.begin; sb < td.end; sb += SUB) {
         const uint32_t lim = (uint32_t)min<int64_t>(SUB, td.end - sb);  // uniform
         Rec rec[IPT];
@@ -826,6 +869,7 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
                 dr[j] = ok ? (d | (rk << 12)) : ~0u;
             }
         }
+        if (xq.q && tid == 0 && sb == td.begin) sh_next = nq;
         __syncthreads();
         const uint32_t total =
             scatter_scan_update<kScatThreads, FMAX / kScatThreads>(cnt, dstart, cur, F, sh16, gof);
@@ -843,7 +887,24 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
         __syncthreads();
         const int64_t nb = sb + SUB;
         const uint32_t nlim = (uint32_t)max<int64_t>(0, min<int64_t>(SUB, td.end - nb));
-        if (nlim > 0) load_sub(nb, nlim);
+        {
+            // the next sub-tile of this tile or, after the last one of an
+            // XCD-local tile, the next tile's first (one load site)
+            int64_t lb = nb;
+            uint32_t ll = nlim;
+            if constexpr (HasTilePrefetch<Src>::value) {
+                if (nlim == 0 && xq.q) {
+                    const uint32_t w = __builtin_amdgcn_readfirstlane(sh_next);
+                    if (w < xq_len) {
+                        tn = __builtin_amdgcn_readfirstlane(xq.q[(size_t)xq_id * xq.stride + w]);
+                        tdn = uniform_tile(tiles, tn);
+                        lb = tdn.begin;
+                        ll = (uint32_t)min<int64_t>(SUB, tdn.end - tdn.begin);
+                    }
+                }
+            }
+            if (ll > 0) load_sub(lb, ll);
+        }
         // write-out in batches of WB staged records per thread, branch-free:
         // slots past the end repeat the last staged record, whose store they
         // duplicate (same value, same address)
@@ -876,6 +937,23 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
         // the next sub-tile's first barrier (after its ranking) orders this
         // write-out's LDS reads before the next scan and staging
     }
+    if (!HasTilePrefetch<Src>::value && xq.q) {
+        // XCD-local without the prefetch: dequeued now, loaded unoverlapped
+        const uint32_t w = __builtin_amdgcn_readfirstlane(sh_next);
+        if (w >= xq_len) break;
+        tn = __builtin_amdgcn_readfirstlane(xq.q[(size_t)xq_id * xq.stride + w]);
+        tdn = uniform_tile(tiles, tn);
+        load_sub(tdn.begin, (uint32_t)min<int64_t>(SUB, tdn.end - tdn.begin));
+    } else if (!xq.q) {
+        it += gridDim.x;
+        if (it >= nt) break;
+        tn = it;
+        tdn = uniform_tile(tiles, tn);
+        load_sub(tdn.begin, (uint32_t)min<int64_t>(SUB, tdn.end - tdn.begin));
+    }
+    if (tn == kNone) break;
+    t = tn;
+    td = tdn;
     }
 }
 

@@ -150,6 +150,52 @@ def test_gpu_partition_levels_and_fallback(built, target, cap):
     assert np.allclose(got["sum"], ref["sum"], rtol=1e-9, atol=1e-9)
 
 
+GLOBAL_MODES = [
+    # MEAN + VARIANCE without SUM: 24-byte ItemV items
+    ("itemv", dict(metrics=[pdp.Metrics.MEAN, pdp.Metrics.VARIANCE, pdp.Metrics.COUNT],
+                   max_partitions_contributed=4, max_contributions_per_partition=2,
+                   min_value=-1.0, max_value=5.0)),
+    # MEAN with SUM: 32-byte Item32 items
+    ("item32", dict(metrics=[pdp.Metrics.MEAN, pdp.Metrics.SUM, pdp.Metrics.PRIVACY_ID_COUNT],
+                    max_partitions_contributed=3, max_contributions_per_partition=2,
+                    min_value=0.0, max_value=10.0)),
+    # PER_PRIVACY_ID bounding with MEAN (Item32)
+    ("per_pid", dict(metrics=[pdp.Metrics.COUNT, pdp.Metrics.SUM, pdp.Metrics.MEAN],
+                     max_contributions=5, min_value=0.0, max_value=10.0)),
+]
+
+
+@pytest.mark.parametrize("name,kw", GLOBAL_MODES, ids=[m[0] for m in GLOBAL_MODES])
+def test_gpu_global_path_item_types(built, monkeypatch, name, kw):
+    """The global-memory bounding kernel (k_bound_big) for the MEAN/VARIANCE
+    item layouts and PER_PRIVACY_ID bounding: every bucket over a 64-record
+    capacity (dpg_set_tuning) and the heavy-id filter off (DPG_NO_HEAVY), so
+    all records take that kernel; partials equal the oracle's
+    (contribution_bounders.py:66-195, combiners.py:382-529)."""
+    monkeypatch.setenv("DPG_NO_HEAVY", "1")
+    P = 3000
+    pid, pk, val = _dataset(31, 200_000, 2_000, P, zipf=1.1)   # ~100 records / pid
+    params = pdp.AggregateParams(**kw)
+    backend = pdp.MI355XBackend(device=0, seed=SEED)
+    backend.ctx.set_tuning(1024, 64)
+    acc = pdp.NaiveBudgetAccountant(1.0, 1e-6)
+    res = pdp.DPEngine(acc, backend).aggregate(
+        pdp.ColumnarData(pid=torch.as_tensor(pid), pk=torch.as_tensor(pk),
+                         value=torch.as_tensor(val), n_partitions=P),
+        params, pdp.DataExtractors("pid", "pk", "value"), public_partitions=list(range(P)))
+    acc.compute_budgets()
+    res.noise_enabled = False
+    res.materialize()
+    ref = oracle.bound_aggregate(pid, pk, val, res.last_bound_fields, SEED,
+                                 public_mask=oracle.bitmap(range(P), P))
+    got = {k: (v.cpu().numpy() if v is not None else None) for k, v in res.last_partials.items()}
+    assert np.array_equal(got["rows"], ref["rows"])
+    assert np.array_equal(got["count"], ref["count"])
+    for k in ("sum", "nsum", "nsq"):
+        if got[k] is not None:
+            assert np.allclose(got[k], ref[k], rtol=1e-9, atol=1e-9), k
+
+
 def test_gpu_4096_digit_level(built, monkeypatch):
     """A 12-bit second partition level (4096 digits: the scatter variant
     with 48 KB of digit arrays, 4 digits per thread in the digit bases),
