@@ -369,6 +369,18 @@ int dpg_ctx_create_comm(dpg_ctx *ctx, const uint8_t *id, int rank, int nranks);
  * `full`; slice->n_partitions is set to n).  Stream-ordered on `stream`. */
 int dpg_reduce_scatter_partials(dpg_ctx *ctx, const dpg_partials *full, dpg_partials *slice,
                                 int64_t *lo, int64_t *n, void *stream);
+/* The same merge with the host's own collective (MPI, gloo, a TCP ring):
+ * dpg_pack_partials writes the non-null arrays of `full` as float64 in the
+ * reduce-scatter layout pack[rank][array][S] (S = ceil(P / nranks), zero
+ * padded past P; array order rows, count, sum, nsum, nsq; pack holds
+ * nranks * arrays * S doubles); after the host's element-wise sum over ranks
+ * delivers this rank's block part[array][S], dpg_unpack_partials writes it
+ * into `slice` (its non-null arrays name the packed ones) and returns
+ * lo = rank * S, n = min(P, lo + S) - lo.  Stream-ordered on `stream`. */
+int dpg_pack_partials(dpg_ctx *ctx, const dpg_partials *full, int nranks, double *pack,
+                      void *stream);
+int dpg_unpack_partials(dpg_ctx *ctx, const double *part, int64_t n_partitions, int nranks,
+                        int rank, dpg_partials *slice, int64_t *lo, int64_t *n, void *stream);
 
 /* Timing/profiling aid: per-stage device time (ms) of the last
  * dpg_bound_aggregate / dpg_preaggregate / dpg_dataset_histograms call,

@@ -19,7 +19,8 @@ EXPORTED = ("dpg_ctx_create", "dpg_ctx_destroy", "dpg_last_error", "dpg_set_seed
             "dpg_bound_aggregate", "dpg_select_and_noise", "dpg_compact_kept",
             "dpg_last_stage_times", "dpg_stream_seed", "dpg_preaggregate",
             "dpg_utility_analysis", "dpg_dataset_histograms",
-            "dpg_comm_unique_id", "dpg_ctx_create_comm", "dpg_reduce_scatter_partials")
+            "dpg_comm_unique_id", "dpg_ctx_create_comm", "dpg_reduce_scatter_partials",
+            "dpg_pack_partials", "dpg_unpack_partials")
 
 COMM_ID_BYTES = 128  # DPG_COMM_ID_BYTES
 
@@ -183,6 +184,13 @@ def load():
                                                     ctypes.POINTER(ctypes.c_int64),
                                                     ctypes.POINTER(ctypes.c_int64), vp]
         lib.dpg_reduce_scatter_partials.restype = ctypes.c_int
+        lib.dpg_pack_partials.argtypes = [vp, ctypes.POINTER(Partials), ctypes.c_int, vp, vp]
+        lib.dpg_pack_partials.restype = ctypes.c_int
+        lib.dpg_unpack_partials.argtypes = [vp, vp, i64, ctypes.c_int, ctypes.c_int,
+                                            ctypes.POINTER(Partials),
+                                            ctypes.POINTER(ctypes.c_int64),
+                                            ctypes.POINTER(ctypes.c_int64), vp]
+        lib.dpg_unpack_partials.restype = ctypes.c_int
         _lib = lib
         return lib
 
@@ -256,6 +264,19 @@ class Context:
                                                   ctypes.byref(slice_), ctypes.byref(lo),
                                                   ctypes.byref(n), stream)
         self.check(st, "dpg_reduce_scatter_partials")
+        return lo.value, n.value
+
+    def pack_partials(self, full: Partials, nranks: int, pack_ptr, stream):
+        st = self.lib.dpg_pack_partials(self.handle, ctypes.byref(full), nranks, pack_ptr, stream)
+        self.check(st, "dpg_pack_partials")
+
+    def unpack_partials(self, part_ptr, n_partitions: int, nranks: int, rank: int,
+                        slice_: Partials, stream):
+        lo, n = ctypes.c_int64(0), ctypes.c_int64(0)
+        st = self.lib.dpg_unpack_partials(self.handle, part_ptr, n_partitions, nranks, rank,
+                                          ctypes.byref(slice_), ctypes.byref(lo),
+                                          ctypes.byref(n), stream)
+        self.check(st, "dpg_unpack_partials")
         return lo.value, n.value
 
     def select_and_noise(self, partials: Partials, sel: SelectParams, noise: NoiseParams,

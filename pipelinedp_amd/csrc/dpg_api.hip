@@ -1663,6 +1663,89 @@ int dpg_ctx_create_comm(dpg_ctx *ctx, const uint8_t *id, int rank, int nranks) {
     return DPG_OK;
 }
 
+namespace {
+// The non-null arrays of `full` (and their counterparts in `slice`, when
+// given) in the pack order rows, count, sum, nsum, nsq.
+int pack_arrays(dpg_ctx *ctx, const dpg_partials *full, const dpg_partials *slice,
+                PackArrays &pa, UnpackArrays &ua) {
+    const void *src[5] = {full->rows, full->count, full->sum, full->nsum, full->nsq};
+    void *dst[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    if (slice) {
+        dst[0] = slice->rows, dst[1] = slice->count, dst[2] = slice->sum;
+        dst[3] = slice->nsum, dst[4] = slice->nsq;
+    }
+    pa = PackArrays{};
+    ua = UnpackArrays{};
+    for (int k = 0; k < 5; ++k) {
+        if (!src[k]) continue;
+        if (slice && !dst[k]) return fail(ctx, DPG_ERR_INVALID_ARG, "slice lacks an array the partials have");
+        pa.a[pa.n] = src[k];
+        pa.is_int[pa.n] = k < 2;
+        ua.a[ua.n] = dst[k];
+        ua.is_int[ua.n] = k < 2;
+        ++pa.n;
+        ++ua.n;
+    }
+    if (pa.n == 0) return fail(ctx, DPG_ERR_INVALID_ARG, "no partial arrays");
+    return DPG_OK;
+}
+
+int launch_pack(dpg_ctx *ctx, const PackArrays &pa, int64_t P, int R, double *pack, hipStream_t s) {
+    int st = DPG_OK;
+    const int64_t S = (P + R - 1) / R;
+    const int64_t total = S * R;
+    const unsigned blocks = (unsigned)std::min<int64_t>((total + 255) / 256, (int64_t)ctx->n_cu * 16);
+    k_pack_partials<<<blocks, 256, 0, s>>>(pa, P, S, R, pack);
+    LAUNCH_CHECK();
+    return st;
+}
+
+int launch_unpack(dpg_ctx *ctx, const UnpackArrays &ua, const double *part, int64_t P, int R,
+                  int rank, dpg_partials *slice, int64_t *lo, int64_t *n, hipStream_t s) {
+    int st = DPG_OK;
+    const int64_t S = (P + R - 1) / R;
+    const int64_t l = std::min<int64_t>(P, (int64_t)rank * S);
+    const int64_t nl = std::min<int64_t>(P, l + S) - l;
+    if (nl > 0) {
+        const unsigned ub = (unsigned)std::min<int64_t>((nl + 255) / 256, (int64_t)ctx->n_cu * 16);
+        k_unpack_partials<<<ub, 256, 0, s>>>(part, S, nl, ua);
+        LAUNCH_CHECK();
+    }
+    *lo = l;
+    *n = nl;
+    slice->n_partitions = nl;
+    return st;
+}
+}  // namespace
+
+int dpg_pack_partials(dpg_ctx *ctx, const dpg_partials *full, int nranks, double *pack,
+                      void *stream) {
+    if (!ctx || !full || !pack || nranks < 1) return DPG_ERR_INVALID_ARG;
+    const int64_t P = full->n_partitions;
+    if (P <= 0) return fail(ctx, DPG_ERR_INVALID_ARG, "n_partitions must be positive");
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, DPG_ERR_HIP, "hipSetDevice");
+    PackArrays pa;
+    UnpackArrays ua;
+    if (int r = pack_arrays(ctx, full, nullptr, pa, ua)) return r;
+    return launch_pack(ctx, pa, P, nranks, pack, static_cast<hipStream_t>(stream));
+}
+
+int dpg_unpack_partials(dpg_ctx *ctx, const double *part, int64_t n_partitions, int nranks,
+                        int rank, dpg_partials *slice, int64_t *lo, int64_t *n, void *stream) {
+    if (!ctx || !part || !slice || !lo || !n || nranks < 1 || rank < 0 || rank >= nranks)
+        return DPG_ERR_INVALID_ARG;
+    if (n_partitions <= 0) return fail(ctx, DPG_ERR_INVALID_ARG, "n_partitions must be positive");
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, DPG_ERR_HIP, "hipSetDevice");
+    // the slice's non-null arrays name the packed arrays (same order)
+    PackArrays pa;
+    UnpackArrays ua;
+    dpg_partials like = *slice;
+    like.n_partitions = n_partitions;
+    if (int r = pack_arrays(ctx, &like, slice, pa, ua)) return r;
+    return launch_unpack(ctx, ua, part, n_partitions, nranks, rank, slice, lo, n,
+                         static_cast<hipStream_t>(stream));
+}
+
 int dpg_reduce_scatter_partials(dpg_ctx *ctx, const dpg_partials *full, dpg_partials *slice,
                                 int64_t *lo, int64_t *n, void *stream) {
     if (!ctx || !full || !slice || !lo || !n) return DPG_ERR_INVALID_ARG;
@@ -1674,41 +1757,16 @@ int dpg_reduce_scatter_partials(dpg_ctx *ctx, const dpg_partials *full, dpg_part
     int st = DPG_OK;
     const int R = ctx->nranks;
     const int64_t S = (P + R - 1) / R;
-    PackArrays pa{};
-    UnpackArrays ua{};
-    const void *src[5] = {full->rows, full->count, full->sum, full->nsum, full->nsq};
-    void *dst[5] = {slice->rows, slice->count, slice->sum, slice->nsum, slice->nsq};
-    for (int k = 0; k < 5; ++k) {
-        if (!src[k]) continue;
-        if (!dst[k]) return fail(ctx, DPG_ERR_INVALID_ARG, "slice lacks an array the partials have");
-        pa.a[pa.n] = src[k];
-        pa.is_int[pa.n] = k < 2;
-        ua.a[ua.n] = dst[k];
-        ua.is_int[ua.n] = k < 2;
-        ++pa.n;
-        ++ua.n;
-    }
-    if (pa.n == 0) return fail(ctx, DPG_ERR_INVALID_ARG, "no partial arrays");
+    PackArrays pa;
+    UnpackArrays ua;
+    if (int r = pack_arrays(ctx, full, slice, pa, ua)) return r;
     WS(pack, double, "comm.pack", (size_t)R * pa.n * S);
     WS(part, double, "comm.part", (size_t)pa.n * S);
-    const int64_t total = S * R;
-    const unsigned blocks = (unsigned)std::min<int64_t>((total + 255) / 256, (int64_t)ctx->n_cu * 16);
-    k_pack_partials<<<blocks, 256, 0, s>>>(pa, P, S, R, pack);
-    LAUNCH_CHECK();
+    if (int r = launch_pack(ctx, pa, P, R, pack, s)) return r;
     const ncclResult_t e = rccl().reduce_scatter(pack, part, (size_t)pa.n * S, ncclFloat64, ncclSum,
                                                  static_cast<ncclComm_t>(ctx->comm), s);
     if (e != ncclSuccess) return fail(ctx, DPG_ERR_HIP, "ncclReduceScatter: " + rccl_msg(e));
-    const int64_t l = std::min<int64_t>(P, (int64_t)ctx->rank * S);
-    const int64_t nl = std::min<int64_t>(P, l + S) - l;
-    if (nl > 0) {
-        const unsigned ub = (unsigned)std::min<int64_t>((nl + 255) / 256, (int64_t)ctx->n_cu * 16);
-        k_unpack_partials<<<ub, 256, 0, s>>>(part, S, nl, ua);
-        LAUNCH_CHECK();
-    }
-    *lo = l;
-    *n = nl;
-    slice->n_partitions = nl;
-    return DPG_OK;
+    return launch_unpack(ctx, ua, part, P, R, ctx->rank, slice, lo, n, s);
 }
 
 }  // extern "C"

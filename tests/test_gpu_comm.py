@@ -4,7 +4,9 @@ across GPUs.  One GPU here, so one rank: the pack -> ncclReduceScatter ->
 unpack round trip must return the partials unchanged (integer arrays exact
 through float64).  Several ranks go through the same calls with one
 communicator per GPU; RCCL refuses two ranks on one device, so that case
-is covered by the torch.distributed path's tests (test_gpu_multirank.py)."""
+is covered by the torch.distributed path's tests (test_gpu_multirank.py),
+and the pack / unpack layout for several ranks by dpg_pack_partials /
+dpg_unpack_partials (the same kernels, host-summed) below."""
 import os
 
 import numpy as np
@@ -69,3 +71,49 @@ def test_reduce_scatter_without_communicator_fails(built):
     p = _native.Partials(16, t.data_ptr(), t.data_ptr(), None, None, None)
     with pytest.raises(_native.NativeError):
         backend.ctx.reduce_scatter_partials(p, p, None)
+
+
+@pytest.mark.parametrize("R", [2, 3])
+def test_pack_unpack_layout_for_several_ranks(built, R):
+    """the [rank][array][S] layout, the zero padding past P and
+    the rank * S slice offsets of the C-ABI pack equal the torch path's
+    (distributed.reduce_scatter_partials); R emulated ranks' packs summed on
+    the host and unpacked per rank give every rank its slice of the sum."""
+    from pipelinedp_amd import _native
+    backend, parts, P = _aggregate()
+    ctx = backend.ctx
+    dev = parts["rows"].device
+    names = [k for k in ("rows", "count", "sum", "nsum", "nsq") if parts.get(k) is not None]
+    S = (P + R - 1) // R
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    ptr = lambda d, k: d[k].data_ptr() if d.get(k) is not None else None  # noqa: E731
+    # rank r holds the partials scaled by r + 1 (integers stay integers)
+    ranks = [{k: (v * (r + 1)) for k, v in parts.items() if v is not None} for r in range(R)]
+    packs = []
+    for r in range(R):
+        full = _native.Partials(P, *(ptr(ranks[r], k) for k in ("rows", "count", "sum", "nsum",
+                                                                  "nsq")))
+        pack = torch.full((R, len(names), S), -5.0, dtype=torch.float64, device=dev)
+        ctx.pack_partials(full, R, pack.data_ptr(), stream)
+        torch.cuda.synchronize()
+        expect = torch.zeros((len(names), R * S), dtype=torch.float64, device=dev)
+        for j, k in enumerate(names):
+            expect[j, :P] = ranks[r][k].to(torch.float64)
+        expect = expect.view(len(names), R, S).transpose(0, 1)
+        assert torch.equal(pack, expect), r
+        packs.append(pack)
+    total = sum(packs)
+    scale = R * (R + 1) // 2
+    for r in range(R):
+        part = total[r].contiguous()
+        out = {k: torch.full((S,), -7, dtype=parts[k].dtype, device=dev) for k in names}
+        sl = _native.Partials(S, *(ptr(out, k) for k in ("rows", "count", "sum", "nsum", "nsq")))
+        lo, n = ctx.unpack_partials(part.data_ptr(), P, R, r, sl, stream)
+        torch.cuda.synchronize()
+        assert lo == r * S and n == min(P, lo + S) - lo
+        for k in names:
+            want = parts[k][lo:lo + n] * scale
+            if parts[k].dtype == torch.int64:
+                assert torch.equal(out[k][:n], want), (r, k)
+            else:
+                assert torch.allclose(out[k][:n], want, rtol=1e-12, atol=1e-9), (r, k)
