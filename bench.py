@@ -366,7 +366,11 @@ def bench_config5(args):
     t0 = time.perf_counter()
     ev0.record(stream)
     stage_tot = {}
+    reps = run = None
     for _ in range(args.steps):
+        # the previous step's analysis (its ~23 GB of pairs) is released
+        # before the next one allocates: a caller keeps one analysis at a time
+        reps = run = None
         reps, run = step()
         for k, v in run.stage_ms.items():
             stage_tot[k] = stage_tot.get(k, 0.0) + v

@@ -32,6 +32,7 @@
 #include "dpg_partition.h"
 #include "dpg_select.h"
 #include "dpg_sortb.h"
+#include "dpg_sortmw.h"
 #include "dpg_utility.h"
 #include "dpg_wave.h"
 
@@ -639,6 +640,17 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
             pc = std::max(1, std::min(pc, std::atoi(e)));
         return pc;
     };
+    // multi-wave sort kernels (dpg_sortmw.h) for the wide and the medium
+    // chunks; DPG_MW_OFF: the single-wave wide kernel and the hash-table
+    // medium kernel.  Their pid slots need <= 7 hash bits below a bucket.
+    const bool use_mw = use_sort && pl.plb <= 7 && std::getenv("DPG_MW_OFF") == nullptr;
+    auto blocks_per_cu = [&](const void *kern, int threads, size_t lds) {
+        int b = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, threads, lds) != hipSuccess ||
+            b <= 0)
+            b = 1;
+        return b;
+    };
     const void *narrow = nullptr, *wide = nullptr;
     if constexpr (!ItemTraits<Item>::preagg) {
         if (use_sort && !wpk) {
@@ -683,12 +695,13 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     bpl.heavy_fb = hfb;
     bpl.heavy_nfb = &ctl->heavy_nfb;
     if (timing) {
-        WS(pc, unsigned long long, "bound.phase_cyc", 48);
-        HIP_TRY(hipMemsetAsync(pc, 0, 48 * 8, s));
+        WS(pc, unsigned long long, "bound.phase_cyc", 64);
+        HIP_TRY(hipMemsetAsync(pc, 0, 64 * 8, s));
         bpl.phase_cyc = pc;
     }
     // zero-length marker stage: which small-chunk kernel bounded this call
     stage(ctx, s, use_sort ? "bound.kernel=sort" : "bound.kernel=hash");
+    if (use_mw) stage(ctx, s, "bound.multiwave");  // marker: wide / medium chunks in dpg_sortmw.h
     stage(ctx, s, "bound");
     if constexpr (!ItemTraits<Item>::preagg) if (use_sort) {
         WS(defer, uint8_t, "bound.defer", std::max<size_t>(chunk_cap, 1));
@@ -699,15 +712,30 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
             k_bound_sorted<Item, R, false, W><<<Gw, 64, wave_lds, s>>>(
                 recs, refined, hrec, chunk_list, &ctl->n_chunks, bpl, items, wg_off, wg_cnt, defer,
                 Gw);
-            // chunks with more candidates than the narrow kernel sorts
+            // chunks with more candidates than the narrow kernel sorts: two
+            // waves per chunk (4 waves per SIMD) or, DPG_MW_OFF, the
+            // single-wave 8-element kernel (2 waves per SIMD)
             stage(ctx, s, "bound.wide");
-            const uint32_t Gx = std::min<uint32_t>(
-                Gw, (uint32_t)(ctx->n_cu * waves_per_cu(wide, wave_lds)));
             BoundParams bpx = bpl;
             bpx.phase_cyc = nullptr;
-            k_bound_sorted<Item, R, true, W><<<Gx, 64, wave_lds, s>>>(
-                recs, refined, hrec, chunk_list, &ctl->n_chunks, bpx, items, wg_off, wg_cnt, defer,
-                Gw);
+            if (use_mw) {
+                if (timing) bpx.phase_cyc = bpl.phase_cyc + 48;
+                using LW = SortLayoutMW<Item, R, W, 2>;
+                const void *k2 = (const void *)k_bound_sorted_w2<Item, R, W>;
+                (void)hipFuncSetAttribute(k2, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          (int)LW::TOTAL);
+                const uint32_t Gx = std::min<uint32_t>(
+                    Gw, (uint32_t)(ctx->n_cu * blocks_per_cu(k2, LW::T, LW::TOTAL)));
+                k_bound_sorted_w2<Item, R, W><<<Gx, LW::T, LW::TOTAL, s>>>(
+                    recs, refined, hrec, chunk_list, &ctl->n_chunks, bpx, items, wg_off, wg_cnt,
+                    defer, Gw);
+            } else {
+                const uint32_t Gx = std::min<uint32_t>(
+                    Gw, (uint32_t)(ctx->n_cu * waves_per_cu(wide, wave_lds)));
+                k_bound_sorted<Item, R, true, W><<<Gx, 64, wave_lds, s>>>(
+                    recs, refined, hrec, chunk_list, &ctl->n_chunks, bpx, items, wg_off, wg_cnt,
+                    defer, Gw);
+            }
         };
         if (!wpk) {
             launch(std::false_type{});
@@ -725,7 +753,31 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     }
     if (prog) watchdog_wait(s, prog, Gw, "k_bound_waves");
     stage(ctx, s, "bound.medium");
-    if (Gm) {
+    bool medium_done = false;
+    if constexpr (!ItemTraits<Item>::preagg) {
+        if (Gm && use_mw) {
+            auto launch_m = [&](auto wpk_tag) {
+                constexpr bool W = decltype(wpk_tag)::value;
+                using LM = SortLayoutMW<Item, R, W, 4>;
+                (void)hipFuncSetAttribute((const void *)k_bound_sorted_m4<Item, R, W>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)LM::TOTAL);
+                BoundParams bpm = bpl;
+                if (timing) bpm.phase_cyc = bpl.phase_cyc + 16;
+                k_bound_sorted_m4<Item, R, W><<<Gm, LM::T, LM::TOTAL, s>>>(
+                    recs, refined, mchunk_list, &ctl->n_mchunks, bpm, items, wg_off + Gw,
+                    wg_cnt + Gw);
+            };
+            if (!wpk) {
+                launch_m(std::false_type{});
+                medium_done = true;
+            } else if constexpr (sizeof(R) == 12) {
+                launch_m(std::true_type{});
+                medium_done = true;
+            }
+            LAUNCH_CHECK();
+        }
+    }
+    if (Gm && !medium_done) {
         BoundParams bpm = bpl;
         if (timing) bpm.phase_cyc = bpl.phase_cyc + 16;
         if (prog) bpm.progress = prog + Gw;
@@ -738,28 +790,32 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     }
     stage(ctx, s, "bound.tail");
     if (timing) {
-        unsigned long long h[32];
+        unsigned long long h[64];
         HIP_TRY(hipMemcpy(h, bpl.phase_cyc, sizeof(h), hipMemcpyDeviceToHost));
         static const char *nmh[12] = {"A0.cas", "A1.count", "B.slots", "C1.cand", "C2.rank",
                                       "D.state", "E.mcpp", "F.acc", "G.emit", "A.probe",
                                       "Am.pidc", "Am.cand"};
         static const char *nms[12] = {"A.pids+cand", "S.sort", "P.pairs", "M.mcpp", "F.emit",
                                       "end", "-", "-", "-", "-", "-", "-"};
-        const char *const *nmw = use_sort ? nms : nmh;
         static const char *nmc[9] = {"A0.cas", "A1.count", "A2.barrier", "B.slots", "C.mpc",
                                      "D.state", "E.mcpp", "F.acc", "G.emit"};
-        for (int part = 0; part < 2; ++part) {
-            const unsigned long long *hp = h + 16 * part;
-            const uint32_t gg = part ? Gm : Gw;
+        for (int part = 0; part < 3; ++part) {
+            // small chunks, medium chunks, wide chunks (multi-wave kernel);
+            // totals per workgroup of the kernel's own grid size
+            const unsigned long long *hp = h + (part == 2 ? 48 : 16 * part);
+            if (part == 2 && !use_mw) continue;
+            const uint32_t gg = part == 1 ? Gm : Gw;
             if (!gg) continue;
             unsigned long long tot = 0;
-            const int np = part ? 9 : 12;
+            const bool sortnames = part == 0 ? use_sort : use_mw;
+            const int np = sortnames ? 6 : part ? 9 : 12;
             for (int i = 0; i < np; ++i) tot += hp[i];
             std::fprintf(stderr, "[dpg phase] %s chunks=%u over=%u over2=%u per-WG Mcycles:",
-                         part ? "medium" : "small", part ? hctl.n_mchunks : hctl.n_chunks,
-                         hctl.n_over, hctl.n_over2);
+                         part == 2 ? "wide(mw)" : part ? "medium" : "small",
+                         part == 1 ? hctl.n_mchunks : hctl.n_chunks, hctl.n_over, hctl.n_over2);
+            const char *const *nm = sortnames ? nms : part ? nmc : nmh;
             for (int i = 0; i < np; ++i)
-                std::fprintf(stderr, " %s=%.3f(%.0f%%)", (part ? nmc : nmw)[i], hp[i] / 1e6 / gg,
+                std::fprintf(stderr, " %s=%.3f(%.0f%%)", nm[i], hp[i] / 1e6 / gg,
                              100.0 * hp[i] / (tot ? tot : 1));
             std::fprintf(stderr, "\n");
         }
@@ -960,6 +1016,20 @@ int pipeline(dpg_ctx *ctx, hipStream_t s, const int64_t *pid, const int64_t *pk,
 #endif
     const bool l1_grp = env_int("DPG_L1_GRP", DPG_L1_GRP) != 0;
     const bool l2_grp = env_int("DPG_L2_GRP", DPG_L2_GRP) != 0;
+    // level 1 writes every record's level-2 digit beside it (u16), so that
+    // the level-2 histogram reads 2 bytes per record instead of 8
+#ifndef DPG_L2_AUX
+#define DPG_L2_AUX 1
+#endif
+    const uint32_t shift2 = pl.pkbits + (pl.kbits - pl.b1) - pl.b2;
+    uint16_t *aux2 = nullptr;
+    if (pl.b2 > 0 && env_int("DPG_L2_AUX", DPG_L2_AUX) != 0) {
+        WS(ax, uint16_t, "aux2", n);
+        aux2 = ax;
+        s1.aux = ax;
+        s1.aux_shift = shift2;
+        s1.aux_mask = (1u << pl.b2) - 1u;
+    }
     int r = run_level<SrcSoAKey<R>, R, Ipt<R>::L1, 2048>(ctx, s, s1, 1u, nullptr, nullptr,
                                                          &ctl->n_scalar, n, F1, pl.b1, recA,
                                                          "partition1", &bstart, &bcnt, &ctl->ntiles[0],
@@ -970,7 +1040,8 @@ int pipeline(dpg_ctx *ctx, hipStream_t s, const int64_t *pid, const int64_t *pk,
     if (pl.b2 > 0) {
         // ---- level 2: next b2 hash bits inside every level-1 bucket
         const uint32_t F2 = 1u << pl.b2;
-        SrcAoS<R> s2{recA, f, pl.pkbits + (pl.kbits - pl.b1) - pl.b2, F2 - 1};
+        SrcAoS<R> s2{recA, f, shift2, F2 - 1};
+        s2.aux = aux2;
 // Level 2 in XCD-local mode: one-sub-tile tiles, all tiles of a level-1
 // bucket served by one XCD's workgroups at the same time, so the partial
 // lines of their adjacent runs merge in that XCD's L2 before write-back
