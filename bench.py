@@ -316,22 +316,28 @@ def _ua_options(n_side: int = 8):
 
 
 def _ua_cpu_baseline(n_records: int, P: int):
-    """The utility-analysis oracle (numpy/Python, one core) on a small sample
-    of the same generator and the same 64 configurations."""
-    from oracle import utility_oracle as uo
+    """The same 64-configuration sweep on the host: the vectorised numpy
+    restatement (oracle/utility_sweep_np.py: pre-aggregation + every
+    configuration's per-partition keep probability and error terms; the
+    configurations split over the host cores) on a sample of the same
+    generator (100 records per privacy id, P Zipf partitions)."""
+    from oracle import utility_sweep_np as us
     _, mpc, mcpp = _ua_options()
     n_pid = max(1, n_records // 100)
     pid, pk, val = host_sample(n_records, n_pid, P, 7)
     cfgs = [dict(mpc=a, mcpp=b, min_sum=0.0, max_sum=10.0 * b, noise_kind="LAPLACE",
                  strategy="TRUNCATED_GEOMETRIC", pre_threshold=None) for a, b in zip(mpc, mcpp)]
+    workers = min(16, os.cpu_count() or 1)
     t0 = time.perf_counter()
-    pairs = uo.preaggregate(pid.tolist(), pk.tolist(), val.tolist())
-    uo.analyze(pairs, cfgs, ["COUNT", "SUM", "PRIVACY_ID_COUNT"], 1.0, 1e-6, "LAPLACE")
+    pa, _ = us.sweep(pid, pk, val, cfgs, ["COUNT", "SUM", "PRIVACY_ID_COUNT"], 1.0, 1e-6,
+                     workers=workers)
     dt = time.perf_counter() - t0
-    return {"value": n_records / dt, "unit": "records/s", "cores": 1, "kind": "port",
-            "sample": f"{n_records} records, {n_pid} privacy ids, {P} partitions, 64 "
-                      f"configurations; oracle/utility_oracle.py (numpy + Python loops) "
-                      f"pre-aggregation + per-partition + cross-partition, {dt:.1f} s"}
+    return {"value": n_records / dt, "unit": "records/s", "cores": workers, "kind": "port",
+            "sample": f"{n_records} records, {n_pid} privacy ids, {P} Zipf partitions "
+                      f"({len(pa['pk'])} non-empty), 64 configurations; "
+                      f"oracle/utility_sweep_np.py (vectorised numpy, configurations over "
+                      f"{workers} processes): pre-aggregation + per-partition keep "
+                      f"probabilities and error terms (no cross-partition report), {dt:.1f} s"}
 
 
 def bench_config5(args):
@@ -343,7 +349,7 @@ def bench_config5(args):
     if args.gpus != 1:
         raise SystemExit("config5 runs on one GPU (the sweep does not shard)")
     P = args.partitions or 1_000_000
-    cpu = None if args.no_cpu_baseline else _ua_cpu_baseline(20_000, 200)
+    cpu = None if args.no_cpu_baseline else _ua_cpu_baseline(1_000_000, P)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(0)
     pid, pk, val = generate(args.records, args.pids, P, 0, 1, dev)

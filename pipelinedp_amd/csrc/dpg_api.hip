@@ -82,6 +82,9 @@ struct dpg_ctx {
     uint32_t bucket_target = 0;  // 0: kBucketTarget
     uint32_t bucket_cap = kBCap;
     void *comm = nullptr;        // ncclComm_t (dpg_ctx_create_comm)
+    // device flags of the last dpg_bound_aggregate (its internal-error bit is
+    // read at the next synchronising call, dpg_compact_kept)
+    const uint32_t *last_err = nullptr;
     int rank = 0, nranks = 1;
     // pinned staging arena for host -> device uploads (see upload())
     char *stage_buf = nullptr;
@@ -673,7 +676,8 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
                                        : 0u;
     const uint32_t G = Gw + Gm;
     // heavy buckets handed back are counted twice (candidates + bucket)
-    WS(items, Item, "items", std::max<int64_t>(n + (heavy ? (int64_t)n_global * kWCap : 0), 1));
+    const int64_t items_cap = std::max<int64_t>(n + (heavy ? (int64_t)n_global * kWCap : 0), 1);
+    WS(items, Item, "items", items_cap);
     WS(wg_rec, uint32_t, "wg.rec", G + 1);
     WS(wg_off, int64_t, "wg.off", G + 2);
     WS(wg_cnt, uint32_t, "wg.cnt", G + 1);
@@ -882,16 +886,28 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     }
     k_scan_small<<<1, 1024, 0, s>>>(wg_cnt, G + 1, wg_pre, &ctl->item_cursor);
     LAUNCH_CHECK();
-    HIP_TRY(hipMemcpyAsync(&hctl, ctl, sizeof(Control), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    if (hctl.err & 2u) return fail(ctx, DPG_ERR_HIP, "internal hash-table error in bounding");
-    const int64_t n_items = hctl.item_cursor;
+    constexpr bool kPA = ItemTraits<Item>::preagg;
+    int64_t n_items;
+    if constexpr (kPA) {
+        // the caller needs the pair count on return
+        HIP_TRY(hipMemcpyAsync(&hctl, ctl, sizeof(Control), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (hctl.err & 2u) return fail(ctx, DPG_ERR_HIP, "internal hash-table error in bounding");
+        n_items = hctl.item_cursor;
+    } else {
+        // no host round trip: the item levels and the merge size their grids
+        // and buffers by an upper bound (a privacy id keeps at most mpc
+        // pairs, or L records under PER_PRIVACY_ID) and read the count on the
+        // device; the internal-error flag is checked by dpg_compact_kept
+        const uint64_t pairs_per_id = std::max<uint32_t>(1u, per_pid ? bp.L : bp.mpc);
+        n_items = (int64_t)std::min<uint64_t>((uint64_t)items_cap,
+                                              ((uint64_t)1 << pl.kbits) * pairs_per_id);
+    }
     const int64_t P = pl.P;
     constexpr int kItemIpt = sizeof(Item) == 16 ? 8 : 4;
     // the items are partitioned by partition-key range: one level up to 1024
     // ranges, else two (pk >> (rbits + b2), then (pk >> rbits) mod 2^b2) --
     // the final segment index is the range id either way
-    constexpr bool kPA = ItemTraits<Item>::preagg;
     constexpr uint32_t kRB = kPA ? 11u : (uint32_t)kRangeBits;
     const int64_t nranges = (P + (1ll << kRB) - 1) >> kRB;
     int64_t *baseR = nullptr;
@@ -1102,6 +1118,7 @@ int aggregate_impl(dpg_ctx *ctx, const int64_t *pid, const int64_t *pk, const do
     int st = DPG_OK;
     const int64_t P = p->n_partitions;
     WS(ctl, Control, "control", 1);
+    ctx->last_err = &ctl->err;
     HIP_TRY(hipMemsetAsync(ctl, 0, sizeof(Control), s));
     k_set_i64<<<1, 1, 0, s>>>(&ctl->n_scalar, n);
     LAUNCH_CHECK();
@@ -1450,7 +1467,10 @@ int dpg_compact_kept(dpg_ctx *ctx, const uint8_t *keep, const double *out, int64
     k_compact_write<<<nb, kCompactThreads, 0, s>>>(keep, out, P, n_out, bc, kept_ids, kept_out);
     LAUNCH_CHECK();
     HIP_TRY(hipMemcpyAsync(n_kept, tot, 8, hipMemcpyDeviceToHost, s));
+    uint32_t err = 0;
+    if (ctx->last_err) HIP_TRY(hipMemcpyAsync(&err, ctx->last_err, 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
+    if (err & 2u) return fail(ctx, DPG_ERR_HIP, "internal hash-table error in bounding");
     return DPG_OK;
 }
 
@@ -1494,15 +1514,51 @@ int dpg_utility_analysis(dpg_ctx *ctx, const dpg_pair_entry *pairs,
         y.pre_threshold = (int32_t)x.pre_threshold;
         y.threshold = x.threshold;
         y.scale = x.noise_scale;
-        y.table_offset = (int64_t)tabs.size();
+        y.table_offset = 0;
         y.table_len = 0;
         if (!u->public_partitions && x.selection_strategy == DPG_SELECT_TRUNCATED_GEOMETRIC) {
             if (!x.keep_table || x.table_len <= 0)
                 return fail(ctx, DPG_ERR_INVALID_ARG, "truncated geometric needs keep_table");
-            tabs.insert(tabs.end(), x.keep_table, x.keep_table + x.table_len);
+            // one copy of equal tables (a sweep repeats each l0's table)
+            int64_t off = -1;
+            for (int j = 0; j < i && off < 0; ++j)
+                if (hc[j].table_len == x.table_len &&
+                    std::equal(x.keep_table, x.keep_table + x.table_len,
+                               tabs.begin() + hc[j].table_offset))
+                    off = hc[j].table_offset;
+            if (off < 0) {
+                off = (int64_t)tabs.size();
+                tabs.insert(tabs.end(), x.keep_table, x.keep_table + x.table_len);
+            }
+            y.table_offset = off;
             y.table_len = x.table_len;
         }
     }
+    // selection classes: equal keep functions share a column of the LDS
+    // table of k_ua_select
+    std::vector<int32_t> cls(C), cls_rep;
+    for (int i = 0; i < C; ++i) {
+        int k = 0;
+        for (; k < (int)cls_rep.size(); ++k) {
+            const UaConfig &r = hc[cls_rep[k]], &y = hc[i];
+            if (r.strategy == y.strategy && r.pre_threshold == y.pre_threshold &&
+                r.table_offset == y.table_offset && r.table_len == y.table_len &&
+                r.threshold == y.threshold && r.scale == y.scale)
+                break;
+        }
+        if (k == (int)cls_rep.size()) cls_rep.push_back(i);
+        cls[i] = k;
+    }
+    a.n_cls = (int32_t)cls_rep.size();
+    // pi(0 .. npi - 1) per class in <= 32 KB of LDS (4 waves per CU), at
+    // least the exact PMF's 104 counts
+    a.npi = (int32_t)std::max<int64_t>(kPgfB * kPgfNB, (32 * 1024 / 8) / a.n_cls);
+    WS(dcls, int32_t, "ua.cls", C + cls_rep.size());
+    std::vector<int32_t> hcls(cls);
+    hcls.insert(hcls.end(), cls_rep.begin(), cls_rep.end());
+    UPLOAD(dcls, hcls.data(), 4 * hcls.size());
+    a.cls = dcls;
+    a.cls_rep = dcls + C;
     WS(dcfg, UaConfig, "ua.cfg", C);
     UPLOAD(dcfg, hc.data(), sizeof(UaConfig) * C);
     a.cfg = dcfg;
@@ -1541,7 +1597,10 @@ int dpg_utility_analysis(dpg_ctx *ctx, const dpg_pair_entry *pairs,
     } else if (n > 0) {
         stage(ctx, s, "ua.select");
         const unsigned g = (unsigned)std::min<int64_t>(P, (int64_t)ctx->n_cu * 16);
-        k_ua_select<<<g, 64, 0, s>>>(reinterpret_cast<const ItemPA *>(pairs), partition_start, a);
+        const size_t lds = (size_t)a.npi * a.n_cls * 8;
+        (void)hipFuncSetAttribute((const void *)k_ua_select,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        k_ua_select<<<g, 64, lds, s>>>(reinterpret_cast<const ItemPA *>(pairs), partition_start, a);
         LAUNCH_CHECK();
     }
     if (report) {

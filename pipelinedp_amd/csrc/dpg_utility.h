@@ -62,6 +62,13 @@ struct UaArgs {
     uint32_t *bcount;                 // [kUaBuckets] partitions per bucket, then cursors
     int64_t *order;                   // partitions of the output, bucket by bucket
     double *rep;                      // [kUaBuckets][F][C] summed report fields
+    // selection classes: configurations with the same keep function
+    // (strategy, pre-threshold, keep table / threshold / scale) share one
+    // column of the LDS keep-probability table of k_ua_select
+    const int32_t *cls;               // [C] class of each configuration
+    const int32_t *cls_rep;           // [n_cls] a configuration of each class
+    int32_t n_cls;
+    int32_t npi;                      // keep probabilities pi(0 .. npi - 1) in LDS
 };
 
 __device__ __forceinline__ bool bit_of(const uint8_t *m, int64_t k) {
@@ -215,13 +222,6 @@ __device__ __forceinline__ double ua_pi(const UaConfig &cf, const double *tables
     return 0.5 * erfc(-z * 0.70710678118654752440);
 }
 
-// out-of-line copy for the fully unrolled exact-PMF dot product (keeps the
-// unrolled body small, so the coefficient array stays in registers)
-__device__ __attribute__((noinline)) double ua_pi_call(const UaConfig &cf, const double *tables,
-                                                       int64_t i) {
-    return ua_pi(cf, tables, i);
-}
-
 // refined normal approximation (poisson_binomial.py:61-83)
 __device__ __forceinline__ double ua_G(double x, double skew) {
     const double phi = 0.39894228040143267794 * exp(-0.5 * x * x);
@@ -247,12 +247,29 @@ __device__ __forceinline__ void ua_pi_range(const UaConfig &cf, int64_t &i0, int
     }
 }
 
+// The keep probability pi(i) of every selection class for i < npi, built in
+// LDS once per wave ([i][class]): the dot products below read it instead of
+// one dependent global table load per count (those loads bounded the
+// kernel: 61 ms for 64 configurations over 1e6 partitions).
 __global__ __launch_bounds__(64) void k_ua_select(const ItemPA *pairs, const int64_t *pstart,
                                                   UaArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double spi[];
     const int c = (int)__lane_id();
     const int64_t C64 = a.n_configs;
     const bool lane_on = c < a.n_configs;
     const UaConfig cf = a.cfg[lane_on ? c : 0];
+    const int K = a.n_cls, NPI = a.npi;
+    for (int x = c; x < NPI * K; x += 64) {
+        const int i = x / K, kc = x - i * K;
+        spi[x] = ua_pi(a.cfg[a.cls_rep[kc]], a.tables, i);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int my_cls = a.cls[lane_on ? c : 0];
+    auto pi_of = [&](int64_t i) {
+        return i < NPI ? spi[i * K + my_cls] : ua_pi(cf, a.tables, i);
+    };
     int64_t i0, i1;
     ua_pi_range(cf, i0, i1);
     for (int64_t k = blockIdx.x; k < a.P; k += gridDim.x) {
@@ -293,12 +310,12 @@ __global__ __launch_bounds__(64) void k_ua_select(const ItemPA *pairs, const int
             }
 #pragma unroll
             for (int i = 0; i < kPgfB * kPgfNB; ++i)
-                if (i <= n) keep += co[i] * ua_pi_call(cf, a.tables, i);
+                if (i <= n) keep += co[i] * spi[i * K + my_cls];
         } else {
             const double *mm = a.mom + k * kUaMom * C64 + (lane_on ? c : 0);
             const double mean = mm[0], sd = sqrt(mm[C64]);
             if (sd == 0.0) {
-                keep = ua_pi(cf, a.tables, (int64_t)rint(mean));
+                keep = pi_of((int64_t)rint(mean));
             } else {
                 // the refined normal approximation's PMF over [st, en]
                 // (poisson_binomial.py:61-83) dotted with pi; only counts
@@ -316,7 +333,7 @@ __global__ __launch_bounds__(64) void k_ua_select(const ItemPA *pairs, const int
                 double prev = a0 <= a1 ? Gc(a0 - 1) : 0.0;
                 for (int64_t i = a0; i <= a1; ++i) {
                     const double cur = Gc(i);
-                    keep += (cur - prev) * ua_pi(cf, a.tables, i);
+                    keep += (cur - prev) * pi_of(i);
                     prev = cur;
                 }
                 if (en > i1) keep += Gc(en) - Gc(st > i1 ? st - 1 : i1);

@@ -2,6 +2,8 @@
 reference's own known answers (analysis/tests/utility_analysis_test.py,
 per_partition_combiners_test.py, poisson_binomial_test.py) and the host
 logic of pipelinedp_amd.analysis (no GPU)."""
+import math
+
 import numpy as np
 import pytest
 
@@ -138,3 +140,39 @@ def test_oracle_matches_reference_fixture(case):
     assert len(reports) == len(case["reports"])
     for want, got in zip(case["reports"], reports):
         uc.assert_close(want, got, "report", atol=1e-9, rtol=1e-9)
+
+
+def test_vectorised_sweep_matches_oracle():
+    """oracle/utility_sweep_np.py (the config-5 CPU baseline) reproduces the
+    per-partition results of the loop restatement: keep probability (exact
+    PMF and the normal approximation past 100 pairs) and every metric's
+    error terms, for several configurations, serial and on 2 workers."""
+    from oracle import utility_sweep_np as us
+    rng = np.random.default_rng(5)
+    n = 6000
+    pid = rng.integers(0, 400, n)
+    pk = (rng.zipf(1.3, n) - 1) % 60
+    val = rng.uniform(-1.0, 6.0, n)
+    metrics = ["COUNT", "SUM", "PRIVACY_ID_COUNT"]
+    cfgs = [dict(mpc=a, mcpp=b, min_sum=0.0, max_sum=3.0 * b, noise_kind="LAPLACE",
+                 strategy=s, pre_threshold=pre)
+            for a, b, s, pre in [(1, 1, "TRUNCATED_GEOMETRIC", None), (3, 2, "TRUNCATED_GEOMETRIC", 2),
+                                 (8, 4, "LAPLACE_THRESHOLDING", None),
+                                 (2, 3, "GAUSSIAN_THRESHOLDING", None)]]
+    pairs = uo.preaggregate(pid.tolist(), pk.tolist(), val.tolist())
+    assert max(len(v) for v in pairs.values()) > uo.MAX_EXACT  # both PMF paths
+    per, _ = uo.analyze(pairs, cfgs, metrics, 1.0, 1e-6, "LAPLACE")
+    for workers in (1, 2):
+        pa, res = us.sweep(pid, pk, val, cfgs, metrics, 1.0, 1e-6, workers=workers)
+        for i in range(len(cfgs)):
+            for r, k in enumerate(pa["pk"].tolist()):
+                ref = per[(k, i)]
+                assert res[i]["keep"][r] == pytest.approx(
+                    ref["partition_selection_probability_to_keep"], rel=1e-9, abs=1e-12)
+                for me in ref["metric_errors"]:
+                    got = res[i][me["aggregation"]]
+                    for f in ("sum", "clipping_to_min_error", "clipping_to_max_error",
+                              "expected_l0_bounding_error"):
+                        assert got[f][r] == pytest.approx(me[f], rel=1e-9, abs=1e-9), (i, k, f)
+                    assert math.sqrt(got["var_l0_bounding_error"][r]) == pytest.approx(
+                        me["std_l0_bounding_error"], rel=1e-9, abs=1e-9)

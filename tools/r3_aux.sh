@@ -5,7 +5,7 @@ set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/aux
 mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -q -m gpu -k "partition_levels or 4096 or wide_records or large_partition or exactly or wide_and_medium" --timeout 300 --timeout-method thread > $O/parity.log 2>&1 || { echo parity failed; grep -E "^E |FAILED|Error" $O/parity.log | head -30; tail -5 $O/parity.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > $O/parity.log 2>&1 || { echo parity failed; grep -E "^E |FAILED|Error" $O/parity.log | head -30; tail -5 $O/parity.log; exit 1; }
 tail -1 $O/parity.log
 run() {  # name, env...
   local nm=$1; shift
@@ -23,3 +23,7 @@ for f in sorted(glob.glob("gpurun_out/aux/*.json")):
     print(os.path.basename(f)[:-5], round(d["ms_per_step"], 2), " ".join(f"{k}={st[k]:.2f}" for k in ("partition1:hist", "partition1:scatter", "partition2:hist", "partition2:scatter", "bound")))
 PY
 bash tools/r3_phase.sh
+timeout -k 10 600 python -u -m pytest tests/test_gpu_utility.py tests/test_gpu_histograms.py -x -q -m gpu --timeout 300 --timeout-method thread > $O/ua.log 2>&1 || { echo ua tests failed; grep -E "^E |FAILED|Error" $O/ua.log | head -30; tail -5 $O/ua.log; exit 1; }
+tail -1 $O/ua.log
+timeout -k 10 300 python -u tools/ua_timing.py > $O/ua_timing.log 2>&1 || { echo ua timing failed; tail -20 $O/ua_timing.log; exit 1; }
+tail -2 $O/ua_timing.log
