@@ -759,7 +759,10 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     stage(ctx, s, "bound.medium");
     bool medium_done = false;
     if constexpr (!ItemTraits<Item>::preagg) {
-        if (Gm && use_mw) {
+        // the 4-wave medium kernel measured slower than the hash-table one
+        // (config 4 medium 9.8 vs 7.6 ms: a 1024-element sort for ~300
+        // candidates): opt-in
+        if (Gm && use_mw && std::getenv("DPG_MW_MEDIUM") != nullptr) {
             auto launch_m = [&](auto wpk_tag) {
                 constexpr bool W = decltype(wpk_tag)::value;
                 using LM = SortLayoutMW<Item, R, W, 4>;
@@ -811,7 +814,9 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
             const uint32_t gg = part == 1 ? Gm : Gw;
             if (!gg) continue;
             unsigned long long tot = 0;
-            const bool sortnames = part == 0 ? use_sort : use_mw;
+            const bool sortnames =
+                part == 0 ? use_sort
+                          : use_mw && (part == 2 || std::getenv("DPG_MW_MEDIUM") != nullptr);
             const int np = sortnames ? 6 : part ? 9 : 12;
             for (int i = 0; i < np; ++i) tot += hp[i];
             std::fprintf(stderr, "[dpg phase] %s chunks=%u over=%u over2=%u per-WG Mcycles:",
@@ -1032,20 +1037,7 @@ int pipeline(dpg_ctx *ctx, hipStream_t s, const int64_t *pid, const int64_t *pk,
 #endif
     const bool l1_grp = env_int("DPG_L1_GRP", DPG_L1_GRP) != 0;
     const bool l2_grp = env_int("DPG_L2_GRP", DPG_L2_GRP) != 0;
-    // level 1 writes every record's level-2 digit beside it (u16), so that
-    // the level-2 histogram reads 2 bytes per record instead of 8
-#ifndef DPG_L2_AUX
-#define DPG_L2_AUX 1
-#endif
     const uint32_t shift2 = pl.pkbits + (pl.kbits - pl.b1) - pl.b2;
-    uint16_t *aux2 = nullptr;
-    if (pl.b2 > 0 && env_int("DPG_L2_AUX", DPG_L2_AUX) != 0) {
-        WS(ax, uint16_t, "aux2", n);
-        aux2 = ax;
-        s1.aux = ax;
-        s1.aux_shift = shift2;
-        s1.aux_mask = (1u << pl.b2) - 1u;
-    }
     int r = run_level<SrcSoAKey<R>, R, Ipt<R>::L1, 2048>(ctx, s, s1, 1u, nullptr, nullptr,
                                                          &ctl->n_scalar, n, F1, pl.b1, recA,
                                                          "partition1", &bstart, &bcnt, &ctl->ntiles[0],
@@ -1057,7 +1049,6 @@ int pipeline(dpg_ctx *ctx, hipStream_t s, const int64_t *pid, const int64_t *pk,
         // ---- level 2: next b2 hash bits inside every level-1 bucket
         const uint32_t F2 = 1u << pl.b2;
         SrcAoS<R> s2{recA, f, shift2, F2 - 1};
-        s2.aux = aux2;
 // Level 2 in XCD-local mode: one-sub-tile tiles, all tiles of a level-1
 // bucket served by one XCD's workgroups at the same time, so the partial
 // lines of their adjacent runs merge in that XCD's L2 before write-back
@@ -1534,14 +1525,15 @@ int dpg_utility_analysis(dpg_ctx *ctx, const dpg_pair_entry *pairs,
             y.table_len = x.table_len;
         }
     }
-    // selection classes: equal keep functions share a column of the LDS
-    // table of k_ua_select
+    // selection classes: configurations with equal l0 and keep function share
+    // the LDS keep-probability column and the normal-approximation pass of
+    // k_ua_select
     std::vector<int32_t> cls(C), cls_rep;
     for (int i = 0; i < C; ++i) {
         int k = 0;
         for (; k < (int)cls_rep.size(); ++k) {
             const UaConfig &r = hc[cls_rep[k]], &y = hc[i];
-            if (r.strategy == y.strategy && r.pre_threshold == y.pre_threshold &&
+            if (r.mpc == y.mpc && r.strategy == y.strategy && r.pre_threshold == y.pre_threshold &&
                 r.table_offset == y.table_offset && r.table_len == y.table_len &&
                 r.threshold == y.threshold && r.scale == y.scale)
                 break;

@@ -15,8 +15,6 @@
 // drop the level-1 digit) stages it in LDS beside the record.
 #pragma once
 
-#include <utility>
-
 #include "dpg_common.h"
 
 namespace dpg {
@@ -71,27 +69,6 @@ struct HasPairs<Src, decltype((void)Src::kPairs)> {
     static constexpr bool value = Src::kPairs;
 };
 
-// Level-1 sources that can also write the next level's digit of every
-// record as a u16 beside it (aux), and sources whose histogram can read
-// those digits instead of the records (2 bytes per record instead of 8).
-template <class Src, class = void>
-struct HasAux {
-    static constexpr bool value = false;
-};
-template <class Src>
-struct HasAux<Src, decltype((void)Src::kAux)> {
-    static constexpr bool value = Src::kAux;
-};
-
-template <class Src, class = void>
-struct HasAuxHist {
-    static constexpr bool value = false;
-};
-template <class Src>
-struct HasAuxHist<Src, decltype((void)std::declval<Src>().aux, (void)Src::kDigitFromRec)> {
-    static constexpr bool value = Src::kDigitFromRec;
-};
-
 struct TileDesc {
     int64_t begin, end;
     uint32_t seg;
@@ -143,13 +120,6 @@ struct SrcSoAKey {
     uint64_t kmask;      // stored key bits
     uint32_t dshift;     // kbits - b1
     uint32_t *err;
-    // the next level's digit of every record, written beside it (or null)
-    static constexpr bool kAux = true;
-    uint16_t *aux = nullptr;
-    uint32_t aux_shift = 0, aux_mask = 0;
-    __device__ __forceinline__ uint16_t aux_digit(const R &r) const {
-        return (uint16_t)((RecOps<R>::key(r, f) >> aux_shift) & aux_mask);
-    }
 #ifndef DPG_L1_NT
 #define DPG_L1_NT 1  // same-box A/B: level-1 scatter 8.15 -> 7.86 ms
 #endif
@@ -254,9 +224,6 @@ struct SrcAoS {
         }
         ok[0] = ok[1] = true;
     }
-    // this level's digits as written by the previous level (16-byte aligned
-    // array of n u16), or null: the histogram reads them instead
-    const uint16_t *aux = nullptr;
 };
 
 // Items of S per-workgroup regions read as one sequence: element i lives in
@@ -427,47 +394,6 @@ __global__ __launch_bounds__(kPartThreads) void k_hist(Src src_in, const TileDes
     uint32_t *my = lh + copy * F;
     Src src = src_in;  // per-thread copy (sources may cache lookup state)
     constexpr int U = DPG_HIST_U;  // loads per thread in flight per round
-    if constexpr (HasAuxHist<Src>::value) {
-        if (src.aux) {
-            // u16 digits, 8 per 16-byte load: the unaligned head one per
-            // thread, then U8 loads per thread in flight, the tail per digit
-            const uint16_t *ax = src.aux;
-            const int64_t e = td.end;
-            const int64_t b = min(e, (td.begin + 7) & ~(int64_t)7);
-            if (td.begin + tid < b) atomicAdd(&my[ax[td.begin + tid]], 1u);
-            constexpr int U8 = 4;
-            int64_t i = b + 8 * tid;
-            for (; i + 8 * (U8 - 1) * kPartThreads + 7 < e; i += 8 * U8 * kPartThreads) {
-                uint4 w[U8];
-#pragma unroll
-                for (int u = 0; u < U8; ++u)
-                    w[u] = *reinterpret_cast<const uint4 *>(ax + i + 8 * u * kPartThreads);
-#pragma unroll
-                for (int u = 0; u < U8; ++u) {
-                    const uint32_t x[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
-#pragma unroll
-                    for (int h = 0; h < 4; ++h) {
-                        atomicAdd(&my[x[h] & 0xFFFFu], 1u);
-                        atomicAdd(&my[x[h] >> 16], 1u);
-                    }
-                }
-            }
-            for (; i + 7 < e; i += 8 * kPartThreads) {
-                const uint4 w = *reinterpret_cast<const uint4 *>(ax + i);
-                const uint32_t x[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-                for (int h = 0; h < 4; ++h) {
-                    atomicAdd(&my[x[h] & 0xFFFFu], 1u);
-                    atomicAdd(&my[x[h] >> 16], 1u);
-                }
-            }
-            for (; i < e; ++i) atomicAdd(&my[ax[i]], 1u);
-            __syncthreads();
-            for (uint32_t d = tid; d < F; d += kPartThreads)
-                hist[(size_t)t * F + d] = lh[d] + lh[F + d] + lh[2 * F + d] + lh[3 * F + d];
-            return;
-        }
-    }
     if constexpr (HasPairs<Src>::value) {
         if (src.pairs_ok()) {
             // pairs (i even, 16-byte aligned): an odd first record alone,
@@ -1007,13 +933,6 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
             // lines of the runs merge in L2)
 #pragma unroll
             for (int u = 0; u < WB; ++u) *reinterpret_cast<W *>(&out[c1[u] - c2[u] + kc[u]]) = x[u];
-            if constexpr (HasAux<Src>::value) {
-                if (src.aux) {
-#pragma unroll
-                    for (int u = 0; u < WB; ++u)
-                        src.aux[c1[u] - c2[u] + kc[u]] = src.aux_digit(from_words<Rec>(x[u]));
-                }
-            }
         }
         // the next sub-tile's first barrier (after its ranking) orders this
         // write-out's LDS reads before the next scan and staging

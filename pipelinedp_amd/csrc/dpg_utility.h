@@ -62,9 +62,10 @@ struct UaArgs {
     uint32_t *bcount;                 // [kUaBuckets] partitions per bucket, then cursors
     int64_t *order;                   // partitions of the output, bucket by bucket
     double *rep;                      // [kUaBuckets][F][C] summed report fields
-    // selection classes: configurations with the same keep function
+    // selection classes: configurations with the same l0 and keep function
     // (strategy, pre-threshold, keep table / threshold / scale) share one
-    // column of the LDS keep-probability table of k_ua_select
+    // column of the LDS keep-probability table of k_ua_select and one
+    // normal-approximation pass (the moments depend on l0 only)
     const int32_t *cls;               // [C] class of each configuration
     const int32_t *cls_rep;           // [n_cls] a configuration of each class
     int32_t n_cls;
@@ -106,11 +107,17 @@ __global__ __launch_bounds__(64) void k_ua_accumulate(const ItemPA *pairs,
     const int C = a.n_configs;
     const bool lane_on = c < C;
     const UaConfig cf = a.cfg[lane_on ? c : 0];
+    // Per pair and configuration only the terms that depend on both remain
+    // in the loop: COUNT's error terms are those of x = count >= 0 (its
+    // total is the raw count, its clip-to-min error 0), and
+    // PRIVACY_ID_COUNT's (x = 1 for count > 0) follow from the moments at the
+    // flush: total rn - nz, l0 terms -(sum of 1 - p) = e - rn and sum of q =
+    // v, corrected by the pairs of count 0 (pre-aggregated input only).
     double e = 0, v = 0, t = 0, rn = 0, rc = 0;
-    ErrAcc es, ec, ep;
+    ErrAcc es;
+    double cmx = 0, cel = 0, cvl = 0;  // COUNT: clip-to-max, l0 mean, l0 variance
+    double nz = 0, zel = 0, zvl = 0;   // pairs of count 0: number, sum 1 - p, sum q
     es.clear();
-    ec.clear();
-    ep.clear();
     uint32_t cur = pairs[lo].pk;
     bool skip = a.sample_mask && !bit_of(a.sample_mask, cur);
     auto flush = [&](uint32_t pk) {
@@ -127,17 +134,17 @@ __global__ __launch_bounds__(64) void k_ua_accumulate(const ItemPA *pairs,
         ua_put(m + C64, v, atomic);
         ua_put(m + 2 * C64, t, atomic);
         double *o = a.err + (int64_t)pk * a.n_metrics * 5 * C64 + c;
-        auto put5 = [&](const ErrAcc &x) {
-            ua_put(o, x.tot, atomic);
-            ua_put(o + C64, x.cmin, atomic);
-            ua_put(o + 2 * C64, x.cmax, atomic);
-            ua_put(o + 3 * C64, x.el0, atomic);
-            ua_put(o + 4 * C64, x.vl0, atomic);
+        auto put5 = [&](double tot, double cmin, double cmax, double el0, double vl0) {
+            ua_put(o, tot, atomic);
+            ua_put(o + C64, cmin, atomic);
+            ua_put(o + 2 * C64, cmax, atomic);
+            ua_put(o + 3 * C64, el0, atomic);
+            ua_put(o + 4 * C64, vl0, atomic);
             o += 5 * C64;
         };
-        if (a.has_sum) put5(es);
-        if (a.has_count) put5(ec);
-        if (a.has_pid) put5(ep);
+        if (a.has_sum) put5(es.tot, es.cmin, es.cmax, es.el0, es.vl0);
+        if (a.has_count) put5(rc, 0.0, cmx, cel, cvl);
+        if (a.has_pid) put5(rn - nz, 0.0, 0.0, (e - rn) + zel, v - zvl);
     };
     for (int64_t b = lo; b < hi; b += 64) {
         const int64_t i = b + c < hi ? b + c : hi - 1;
@@ -153,8 +160,8 @@ __global__ __launch_bounds__(64) void k_ua_accumulate(const ItemPA *pairs,
                 flush(cur);
                 e = v = t = rn = rc = 0.0;
                 es.clear();
-                ec.clear();
-                ep.clear();
+                cmx = cel = cvl = 0.0;
+                nz = zel = zvl = 0.0;
                 cur = pk;
                 skip = a.sample_mask && !bit_of(a.sample_mask, cur);
             }
@@ -163,21 +170,41 @@ __global__ __launch_bounds__(64) void k_ua_accumulate(const ItemPA *pairs,
             const uint32_t ilo = __builtin_amdgcn_readlane((uint32_t)inv_bits, j);
             const uint32_t ihi = __builtin_amdgcn_readlane((uint32_t)(inv_bits >> 32), j);
             const double inv = __longlong_as_double((long long)(((uint64_t)ihi << 32) | ilo));
-            const uint32_t slo = __builtin_amdgcn_readlane((uint32_t)__double_as_longlong(mine.sum), j);
-            const uint32_t shi =
-                __builtin_amdgcn_readlane((uint32_t)(__double_as_longlong(mine.sum) >> 32), j);
-            const double s = __longlong_as_double((long long)(((uint64_t)shi << 32) | slo));
             // l0 keep probability of this pair (per_partition_combiners.py:203-205)
             const double p = fmin(1.0, cf.mpc * inv);
-            const double q = p * (1.0 - p);
+            const double omp = 1.0 - p;
+            const double q = p * omp;
             e += p;
             v += q;
             t += q * (1.0 - 2.0 * p);
             rn += 1.0;
             rc += (double)cnt;
-            if (a.has_sum) es.add(s, cf.lo, cf.hi, p, q);
-            if (a.has_count) ec.add((double)cnt, 0.0, cf.mcpp, p, q);
-            if (a.has_pid) ep.add(cnt > 0 ? 1.0 : 0.0, 0.0, 1.0, p, q);
+            if (a.has_sum) {
+                const uint32_t slo =
+                    __builtin_amdgcn_readlane((uint32_t)__double_as_longlong(mine.sum), j);
+                const uint32_t shi =
+                    __builtin_amdgcn_readlane((uint32_t)(__double_as_longlong(mine.sum) >> 32), j);
+                const double x = __longlong_as_double((long long)(((uint64_t)shi << 32) | slo));
+                const double pc = x < cf.lo ? cf.lo : (x > cf.hi ? cf.hi : x);
+                const double d = pc - x;
+                es.tot += x;
+                es.cmin += x < cf.lo ? d : 0.0;
+                es.cmax += x > cf.hi ? d : 0.0;
+                es.el0 -= pc * omp;
+                es.vl0 += pc * pc * q;
+            }
+            if (a.has_count) {
+                const double x = (double)cnt;
+                const double pc = x > cf.mcpp ? cf.mcpp : x;
+                cmx += pc - x;
+                cel -= pc * omp;
+                cvl += pc * pc * q;
+            }
+            if (a.has_pid && cnt == 0) {  // wave-uniform (the pair is broadcast)
+                nz += 1.0;
+                zel += omp;
+                zvl += q;
+            }
         }
     }
     flush(cur);
@@ -267,11 +294,7 @@ __global__ __launch_bounds__(64) void k_ua_select(const ItemPA *pairs, const int
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const int my_cls = a.cls[lane_on ? c : 0];
-    auto pi_of = [&](int64_t i) {
-        return i < NPI ? spi[i * K + my_cls] : ua_pi(cf, a.tables, i);
-    };
-    int64_t i0, i1;
-    ua_pi_range(cf, i0, i1);
+    const int my_sel = lane_on ? my_cls : -1;
     for (int64_t k = blockIdx.x; k < a.P; k += gridDim.x) {
         const int64_t b = pstart[k], n = pstart[k + 1] - b;
         if (n == 0 || (a.sample_mask && !bit_of(a.sample_mask, k))) continue;
@@ -312,31 +335,52 @@ __global__ __launch_bounds__(64) void k_ua_select(const ItemPA *pairs, const int
             for (int i = 0; i < kPgfB * kPgfNB; ++i)
                 if (i <= n) keep += co[i] * spi[i * K + my_cls];
         } else {
-            const double *mm = a.mom + k * kUaMom * C64 + (lane_on ? c : 0);
-            const double mean = mm[0], sd = sqrt(mm[C64]);
-            if (sd == 0.0) {
-                keep = pi_of((int64_t)rint(mean));
-            } else {
-                // the refined normal approximation's PMF over [st, en]
-                // (poisson_binomial.py:61-83) dotted with pi; only counts
-                // with 0 < pi < 1 are evaluated one by one: below i0 pi is 0,
-                // above i1 it is 1 and the remaining mass telescopes to
-                // G(en) - G(i1) (the same sum of CDF differences)
-                const double skew = mm[2 * C64] / (sd * sd * sd);
-                const int64_t st = (int64_t)fmax(0.0, floor(mean - 8.0 * sd));
-                const int64_t en = (int64_t)fmin((double)n, rint(mean + 8.0 * sd));
-                auto Gc = [&](int64_t i) {
-                    return fmin(1.0, fmax(0.0, ua_G(((double)i + 0.5 - mean) / sd, skew)));
+            // refined normal approximation (poisson_binomial.py:61-83): its
+            // PMF over [st, en] dotted with pi.  The moments and pi depend on
+            // the selection class only, so each class is evaluated once with
+            // the wave's lanes over the counts (lane = count, 64 at a time)
+            // instead of once per configuration lane; counts with 0 < pi < 1
+            // are evaluated one by one (below i0 pi is 0, above i1 it is 1
+            // and the remaining mass telescopes to G(en) - G(i1)).
+            for (int kc = 0; kc < K; ++kc) {
+                const int rc = a.cls_rep[kc];
+                const UaConfig cr = a.cfg[rc];
+                const double *mm = a.mom + k * kUaMom * C64 + rc;
+                const double mean = mm[0], sd = sqrt(mm[C64]);
+                double kp;
+                auto pi_k = [&](int64_t i) {
+                    return i < NPI ? spi[i * K + kc] : ua_pi(cr, a.tables, i);
                 };
-                const int64_t a0 = st > i0 ? st : i0;
-                const int64_t a1 = en < i1 ? en : i1;
-                double prev = a0 <= a1 ? Gc(a0 - 1) : 0.0;
-                for (int64_t i = a0; i <= a1; ++i) {
-                    const double cur = Gc(i);
-                    keep += (cur - prev) * pi_of(i);
-                    prev = cur;
+                if (sd == 0.0) {
+                    kp = pi_k((int64_t)rint(mean));
+                } else {
+                    const double skew = mm[2 * C64] / (sd * sd * sd);
+                    const int64_t st = (int64_t)fmax(0.0, floor(mean - 8.0 * sd));
+                    const int64_t en = (int64_t)fmin((double)n, rint(mean + 8.0 * sd));
+                    auto Gc = [&](int64_t i) {
+                        return fmin(1.0, fmax(0.0, ua_G(((double)i + 0.5 - mean) / sd, skew)));
+                    };
+                    int64_t r0, r1;
+                    ua_pi_range(cr, r0, r1);
+                    const int64_t a0 = st > r0 ? st : r0;
+                    const int64_t a1 = en < r1 ? en : r1;
+                    double part = 0.0, carry = 0.0;
+                    // points j = a0 - 1 .. a1: G(j); count j >= a0 adds
+                    // (G(j) - G(j - 1)) pi(j)
+                    for (int64_t j0 = a0 - 1; j0 <= a1; j0 += 64) {
+                        const int64_t j = j0 + c;
+                        const double g = j <= a1 ? Gc(j) : 0.0;
+                        double gp = __shfl_up(g, 1, 64);
+                        if (c == 0) gp = carry;
+                        if (j >= a0 && j <= a1) part += (g - gp) * pi_k(j);
+                        carry = __shfl(g, 63, 64);
+                    }
+#pragma unroll
+                    for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+                    kp = a0 <= a1 ? part : 0.0;
+                    if (en > r1) kp += Gc(en) - Gc(st > r1 ? st - 1 : r1);
                 }
-                if (en > i1) keep += Gc(en) - Gc(st > i1 ? st - 1 : i1);
+                if (my_sel == kc) keep = kp;
             }
         }
         if (lane_on) a.keep[k * C64 + c] = keep;

@@ -441,7 +441,7 @@ MW_MODES = [m for m in MODES if m[0] in ("cross_and_per", "mean_var", "count_onl
 
 
 @pytest.mark.parametrize("name,kw", MW_MODES, ids=[m[0] for m in MW_MODES])
-@pytest.mark.parametrize("mw", ["multiwave", "single"])
+@pytest.mark.parametrize("mw", ["multiwave", "default", "single"])
 def test_gpu_wide_and_medium_chunks_match_oracle(built, monkeypatch, name, kw, mw):
     """Chunks of more than 256 candidate records (two 200-record privacy ids
     per chunk, mpc 100: the pre-filter passes almost everything) and medium
@@ -449,11 +449,14 @@ def test_gpu_wide_and_medium_chunks_match_oracle(built, monkeypatch, name, kw, m
     multi-wave sort kernels (dpg_sortmw.h: 2 waves per wide chunk, 4 per
     medium chunk) -- and, DPG_MW_OFF, through the single-wave 8-element
     kernel and the hash-table medium kernel -- keep exactly the oracle's
-    records."""
+    records.  The default is the 2-wave wide kernel with the hash-table
+    medium kernel (DPG_MW_MEDIUM=1 adds the 4-wave one)."""
+    monkeypatch.delenv("DPG_MW_OFF", raising=False)
+    monkeypatch.delenv("DPG_MW_MEDIUM", raising=False)
     if mw == "single":
         monkeypatch.setenv("DPG_MW_OFF", "1")
-    else:
-        monkeypatch.delenv("DPG_MW_OFF", raising=False)
+    elif mw == "multiwave":
+        monkeypatch.setenv("DPG_MW_MEDIUM", "1")
     rng = np.random.default_rng(77)
     P = 2000
     pid = np.concatenate([np.repeat(np.arange(6000), 200), np.repeat(np.arange(6000, 6300), 700)])
@@ -472,7 +475,7 @@ def test_gpu_wide_and_medium_chunks_match_oracle(built, monkeypatch, name, kw, m
     res.noise_enabled = False
     res.materialize()
     st = backend.ctx.stage_times()
-    assert ("bound.multiwave" in st) == (mw == "multiwave")
+    assert ("bound.multiwave" in st) == (mw != "single")
     assert st["bound.wide"] > 0.0 and st["bound.medium"] > 0.0
     plan = res.plan
     ref = oracle.bound_aggregate(pid, pk, val if plan.needs_values() else None,
