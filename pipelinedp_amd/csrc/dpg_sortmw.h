@@ -194,7 +194,6 @@ __device__ __forceinline__ int mw_sort_chunk(uint32_t nc, char *smem, const Boun
                                               Item *items, uint32_t &nitems, PhaseTimer &clk) {
     using L = SortLayoutMW<Item, R, kWPk, NW>;
     constexpr int T = L::T, CAP = L::CAP, PB = L::PB;
-    constexpr bool kLex = kWPk;
     constexpr bool kVar = ItemTraits<Item>::var;
     constexpr bool kSum = ItemTraits<Item>::sum;
     const uint8_t *cpkl = reinterpret_cast<const uint8_t *>(smem + L::CPKL);
@@ -225,17 +224,43 @@ __device__ __forceinline__ int mw_sort_chunk(uint32_t nc, char *smem, const Boun
     // ---- S: sort (key, record index | kWPk: position | low pk bits << PB)
     uint64_t k[4];
     uint32_t o[4];
+    auto load = [&]() {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const uint32_t i = 4 * tid + j;
-        const uint32_t ic = min(i, (uint32_t)CAP - 1);
-        const uint64_t x = ckey[ic];
-        const uint32_t y = kWPk ? (ic | ((uint32_t)cpkl[ic] << PB)) : cidx[ic];
-        k[j] = i < nc ? x : kSkPad;
-        o[j] = i < nc ? y : 0u;
-    }
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t i = 4 * tid + j;
+            const uint32_t ic = min(i, (uint32_t)CAP - 1);
+            const uint64_t x = ckey[ic];
+            const uint32_t y = kWPk ? (ic | ((uint32_t)cpkl[ic] << PB)) : cidx[ic];
+            k[j] = i < nc ? x : kSkPad;
+            o[j] = i < nc ? y : 0u;
+        }
+    };
+    load();
     for (uint32_t q = tid; q < kWCq; q += T) full[q] = 0;
-    mw_sort<NW, kLex>(k, o, xk, xo);
+    // by key only; wide partition keys (kWPk) whose low bits ride in the
+    // payload re-sort by (key, payload) when two pairs of one pid share a
+    // key (same priority and top 24 pk bits, ~2^-56 per pair of pairs):
+    // the lexicographic comparator costs the common case a third more
+    mw_sort<NW, false>(k, o, xk, xo);
+    if constexpr (kWPk) {
+        xk[tid] = k[3];
+        xo[tid] = o[3];
+        __syncthreads();
+        const uint64_t pk0 = tid ? xk[tid - 1] : 0ull;
+        const uint32_t po0 = tid ? xo[tid - 1] : 0u;
+        bool coll = false;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t i = 4 * tid + j;
+            const uint64_t pv = j ? k[j - 1] : pk0;
+            const uint32_t pvo = j ? o[j - 1] : po0;
+            coll |= i < nc && i > 0 && k[j] == pv && (o[j] >> PB) != (pvo >> PB);
+        }
+        if (mw_any<NW>(coll, scr)) {
+            load();
+            mw_sort<NW, true>(k, o, xk, xo);
+        }
+    }
     mark(bp, 1, clk);
 
     // ---- P: pair starts, ordinals, rank inside the pid
