@@ -254,6 +254,17 @@ __global__ void k_pid_minmax(const int64_t *pid, int64_t n, unsigned long long *
     }
 }
 
+// Levels of at most this many digit bits rank with wave-aggregated LDS
+// atomics (one per distinct digit per wave) instead of one per record;
+// DPG_AGG_BITS overrides it for experiments.
+int agg_bits() {
+    static const int v = [] {
+        const char *e = std::getenv("DPG_AGG_BITS");
+        return e ? std::atoi(e) : 4;
+    }();
+    return v;
+}
+
 // One partition level in grouped XCD-local mode: digit histograms per group
 // (level 1: G consecutive sub-tiles of the input, G = the CUs of one XCD;
 // later levels: one group per segment), every group's sub-tiles scattered
@@ -319,7 +330,7 @@ int run_level_grouped(dpg_ctx *ctx, hipStream_t s, const Src &src, uint32_t S,
     LAUNCH_CHECK();
     constexpr size_t lds = scatter_lds<Src, Rec, IPT, FMAX>();
     static_assert(lds <= 160 * 1024, "scatter LDS");
-    auto kern = bits > 4 ? k_scatter<Src, Rec, IPT, FMAX, false> : k_scatter<Src, Rec, IPT, FMAX, true>;
+    auto kern = bits > agg_bits() ? k_scatter<Src, Rec, IPT, FMAX, false> : k_scatter<Src, Rec, IPT, FMAX, true>;
     (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
     stage(ctx, s, (t + ":scatter").c_str());
@@ -404,7 +415,7 @@ int run_level(dpg_ctx *ctx, hipStream_t s, const Src &src, uint32_t S, const int
     constexpr size_t lds = scatter_lds<Src, Rec, IPT, FMAX>();
     static_assert(lds <= 160 * 1024, "scatter LDS");
     // few digits: wave-aggregated ranking; otherwise one LDS atomic per record
-    auto kern = bits > 4 ? k_scatter<Src, Rec, IPT, FMAX, false> : k_scatter<Src, Rec, IPT, FMAX, true>;
+    auto kern = bits > agg_bits() ? k_scatter<Src, Rec, IPT, FMAX, false> : k_scatter<Src, Rec, IPT, FMAX, true>;
     (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
     stage(ctx, s, (t + ":scatter").c_str());

@@ -50,6 +50,9 @@ namespace dpg {
 constexpr float kSortCandC = 1.5f;  // same-box A/B, config 2 bound: 2.0 9.03 ms, 1.5 7.49, 1.25 7.47 + more restarts
 
 constexpr uint32_t kSkPkBits = 24;  // partition-key bits of the sort key
+#ifndef DPG_SORT_PACKED
+#define DPG_SORT_PACKED 1  // narrow kernel: keys with the position packed in, no payload
+#endif
 constexpr uint64_t kSkPad = ~0ull;  // padding elements (real keys have bit 63 clear)
 
 // The wave's LDS working set is kept under 10 KB (COUNT / SUM items) so that
@@ -217,6 +220,61 @@ __device__ __forceinline__ void bitonic_sort(uint64_t (&k)[E], uint32_t (&o)[E])
     }
 }
 
+// The same network over keys alone (unique keys: the candidate position
+// rides in the low bits, see sort_chunk).
+template <int E>
+__device__ __forceinline__ void bitonic_sort_keys(uint64_t (&k)[E]) {
+    constexpr int LOG_S = E == 1 ? 6 : E == 2 ? 7 : E == 4 ? 8 : 9;
+    constexpr int LOG_E = LOG_S - 6;
+    uint32_t lid = __lane_id();
+    asm volatile("" : "+v"(lid));
+    auto cex = [&](int j, int j2) {
+        const uint64_t a = k[j], b = k[j2];
+        k[j] = a < b ? a : b;
+        k[j2] = a < b ? b : a;
+    };
+#pragma unroll
+    for (int lk = 1; lk <= LOG_S; ++lk) {
+        const int kk = 1 << lk;
+        if (lk <= LOG_E) {
+#pragma unroll
+            for (int j = 0; j < E; ++j) {
+                const int j2 = j ^ (kk - 1);
+                if (j < j2) cex(j, j2);
+            }
+        } else {
+            const int m = (kk >> LOG_E) - 1;
+            const bool lower = (lid & (uint32_t)((m + 1) >> 1)) == 0;
+            uint64_t y[E];
+#pragma unroll
+            for (int j = 0; j < E; ++j) y[j] = xlane64(k[E - 1 - j], m);
+#pragma unroll
+            for (int j = 0; j < E; ++j) {
+                const bool take = lower ? y[j] < k[j] : k[j] < y[j];
+                k[j] = take ? y[j] : k[j];
+            }
+        }
+#pragma unroll
+        for (int ls = lk - 2; ls >= 0; --ls) {
+            const int sd = 1 << ls;
+            if (ls < LOG_E) {
+#pragma unroll
+                for (int j = 0; j < E; ++j)
+                    if (!(j & sd)) cex(j, j | sd);
+            } else {
+                const int m = sd >> LOG_E;
+                const bool lower = (lid & (uint32_t)m) == 0;
+#pragma unroll
+                for (int j = 0; j < E; ++j) {
+                    const uint64_t y = xlane64(k[j], m);
+                    const bool take = lower ? y < k[j] : k[j] < y;
+                    k[j] = take ? y : k[j];
+                }
+            }
+        }
+    }
+}
+
 // Sorts the nc candidates and bounds them (phases S, P, M, F of the header).
 // Returns kRoundRestart when the chunk must restart: the filtered pids short
 // of mpc candidate pairs have had their bound lifted (their CBND set to
@@ -274,7 +332,55 @@ __device__ __forceinline__ int sort_chunk(uint32_t nc, char *smem, const BoundPa
     }
     full[lane] = 0;
     full[lane + 64u] = 0;
-    bitonic_sort<E, kLex>(k, o);
+    bool sorted_packed = false;
+    if constexpr (!kWPk && !kLex && E <= 4 && DPG_SORT_PACKED) {
+        // keys alone (5 instead of 7 VALU per compare-exchange): pid slot (7
+        // bits) | top 48 - pkbits bits of the pair priority | pk | candidate
+        // position (9 bits); the full keys and record indices are read back
+        // by position.  Two pairs of one pid whose priorities agree in the
+        // kept bits (~24^2 / 2^29 per pid at pkbits 20) may come out in pk
+        // order instead of priority order: the full keys are then not
+        // ascending and the chunk is sorted again with key and payload.
+        const uint32_t pkb = f.pkbits;
+        const uint32_t ppb = 48u - pkb;
+        const uint64_t pkm = (1ull << pkb) - 1ull;
+        uint64_t pk64[E];
+#pragma unroll
+        for (int j = 0; j < E; ++j) {
+            const uint32_t i = lane * E + j;
+            const uint64_t x = k[j];
+            const uint64_t pp = (x >> kSkPkBits) & 0xFFFFFFFFull;
+            pk64[j] = i < nc ? (((x >> 56) << 57) | ((pp >> (32u - ppb)) << (9u + pkb)) |
+                                ((x & pkm) << 9) | (uint64_t)i)
+                             : kSkPad;
+        }
+        bitonic_sort_keys<E>(pk64);
+#pragma unroll
+        for (int j = 0; j < E; ++j) {
+            const uint32_t i = lane * E + j;
+            const uint32_t pos = (uint32_t)pk64[j] & 511u;
+            k[j] = i < nc ? ckey[min(pos, (uint32_t)kWCap - 1)] : kSkPad;
+            o[j] = i < nc ? cidx[min(pos, (uint32_t)kWCap - 1)] : 0u;
+        }
+        const uint64_t pl = (uint64_t)__shfl_up((long long)k[E - 1], 1, 64);
+        bool bad = false;
+#pragma unroll
+        for (int j = 0; j < E; ++j) {
+            const uint32_t i = lane * E + j;
+            bad |= i > 0 && i < nc && k[j] < (j ? k[j - 1] : pl);
+        }
+        sorted_packed = __ballot(bad) == 0;
+        if (!sorted_packed) {
+#pragma unroll
+            for (int j = 0; j < E; ++j) {
+                const uint32_t i = lane * E + j;
+                const uint32_t ic = min(i, (uint32_t)kWCap - 1);
+                k[j] = i < nc ? ckey[ic] : kSkPad;
+                o[j] = i < nc ? cidx[ic] : 0u;
+            }
+        }
+    }
+    if (!sorted_packed) bitonic_sort<E, kLex>(k, o);
     mark(bp, 1, clk);
 
     // ---- P: pair starts, ordinals, rank inside the pid
