@@ -286,8 +286,15 @@ int run_level_grouped(dpg_ctx *ctx, hipStream_t s, const Src &src, uint32_t S,
 #ifndef DPG_L1_GROUP
 #define DPG_L1_GROUP 1
 #endif
+    // later levels: one group per segment, or (DPG_SEG_GROUP, experiments)
+    // groups of that many records, rounded to whole sub-tiles
+    static const int64_t seg_group = [] {
+        const char *e = std::getenv("DPG_SEG_GROUP");
+        return e ? std::max<int64_t>(0, std::atoll(e)) : (int64_t)0;
+    }();
     const int64_t gsz = single ? sub * std::max<int64_t>(1, DPG_L1_GROUP * ctx->n_cu / 8)
-                               : ((int64_t)1 << 40);  // one group per segment
+                        : seg_group > 0 ? std::max<int64_t>(1, seg_group / sub) * sub
+                                        : ((int64_t)1 << 40);
     const uint32_t max_groups = (uint32_t)(n_upper / std::min<int64_t>(gsz, n_upper + 1) + S + 1);
     const uint32_t max_subs = (uint32_t)(n_upper / sub + max_groups + 1);
     std::string t(tag);
