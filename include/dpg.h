@@ -165,6 +165,10 @@ typedef struct dpg_select_params {
                                     (indexed by local partition id)        */
     uint64_t nonce;              /* per-release nonce of the selection and
                                     noise draws (see dpg_bound_params)      */
+    int64_t pk_stride;           /* global pk of partials index i is
+                                    pk_offset + i * pk_stride (multi-GPU
+                                    slices are interleaved: rank r owns
+                                    r, r + R, ...); <= 0 means 1            */
 } dpg_select_params;
 
 typedef struct dpg_noise_params {
@@ -362,25 +366,43 @@ int dpg_dataset_histograms(dpg_ctx *ctx, const dpg_pair_entry *pairs, int64_t n_
 #define DPG_COMM_ID_BYTES 128
 int dpg_comm_unique_id(uint8_t *id);
 int dpg_ctx_create_comm(dpg_ctx *ctx, const uint8_t *id, int rank, int nranks);
-/* Sums the dense partials of every rank (ONE ncclReduceScatter of all
- * non-null arrays packed as float64 -- exact below 2^53) and writes this
- * rank's slice [lo, lo + n), lo = rank * S, S = ceil(P / nranks), into
- * `slice` (its arrays hold >= S entries; the same arrays non-null as in
- * `full`; slice->n_partitions is set to n).  Stream-ordered on `stream`. */
+/* Partition ownership is interleaved: rank r owns the partitions
+ * r, r + R, r + 2R, ... (R = nranks), so hot low partition ids spread over
+ * every rank; slice element i is partition lo + i * R with lo = r.
+ * The merge also carries each rank's internal-error flag (a bounding whose
+ * hash table overflowed, dpg_compact_kept's error): every rank receives the
+ * sum of all flags and latches it, so a failure on any rank fails the
+ * dpg_compact_kept of every rank instead of releasing partials of a
+ * mis-bounded shard.
+ *
+ * dpg_reduce_scatter_partials sums the dense partials of every rank (ONE
+ * ncclReduceScatter of all non-null arrays packed as float64 -- exact below
+ * 2^53) and writes this rank's slice (n = number of partitions = r mod R
+ * in [0, P)) into `slice` (its arrays hold >= S = ceil(P / R) entries; the
+ * same arrays non-null as in `full`; slice->n_partitions is set to n).
+ * Stream-ordered on `stream`. */
 int dpg_reduce_scatter_partials(dpg_ctx *ctx, const dpg_partials *full, dpg_partials *slice,
                                 int64_t *lo, int64_t *n, void *stream);
 /* The same merge with the host's own collective (MPI, gloo, a TCP ring):
  * dpg_pack_partials writes the non-null arrays of `full` as float64 in the
- * reduce-scatter layout pack[rank][array][S] (S = ceil(P / nranks), zero
- * padded past P; array order rows, count, sum, nsum, nsq; pack holds
- * nranks * arrays * S doubles); after the host's element-wise sum over ranks
- * delivers this rank's block part[array][S], dpg_unpack_partials writes it
- * into `slice` (its non-null arrays name the packed ones) and returns
- * lo = rank * S, n = min(P, lo + S) - lo.  Stream-ordered on `stream`. */
+ * reduce-scatter layout pack[rank][B], B = arrays * S + 1: [array][S] with
+ * element i = partition i * R + rank (zero past P; array order rows, count,
+ * sum, nsum, nsq), then this rank's error flag (pack holds nranks * B
+ * doubles); after the host's element-wise sum over ranks delivers this
+ * rank's block part[B], dpg_unpack_partials writes it into `slice` (its
+ * non-null arrays name the packed ones), latches a nonzero error sum and
+ * returns lo = rank and n.  Stream-ordered on `stream`. */
 int dpg_pack_partials(dpg_ctx *ctx, const dpg_partials *full, int nranks, double *pack,
                       void *stream);
 int dpg_unpack_partials(dpg_ctx *ctx, const double *part, int64_t n_partitions, int nranks,
                         int rank, dpg_partials *slice, int64_t *lo, int64_t *n, void *stream);
+/* The error flag alone, for a merge the host routes itself (e.g. a sparse
+ * all-to-all of the occupied partitions): dpg_export_error writes 1.0 to
+ * device *dst if the context's last bounding latched an internal error, else
+ * 0.0; dpg_import_error latches the error if any of the n device doubles at
+ * src is nonzero.  Both stream-ordered, no host synchronisation. */
+int dpg_export_error(dpg_ctx *ctx, double *dst, void *stream);
+int dpg_import_error(dpg_ctx *ctx, const double *src, int64_t n, void *stream);
 
 /* Timing/profiling aid: per-stage device time (ms) of the last
  * dpg_bound_aggregate / dpg_preaggregate / dpg_dataset_histograms call,

@@ -416,8 +416,9 @@ int dpo_select_and_noise(uint64_t seed, const dpg_partials *in,
                          uint8_t *keep, double *out) {
     seed = dpo_stream_seed(seed, s->nonce);
     int64_t P = in->n_partitions;
+    const int64_t stride = s->pk_stride > 0 ? s->pk_stride : 1;
     for (int64_t k = 0; k < P; ++k) {
-        uint64_t gk = (uint64_t)(k + s->pk_offset);
+        uint64_t gk = (uint64_t)(s->pk_offset + k * stride);
         int kp = keep_partition(s, seed, gk, k, in->rows[k]);
         keep[k] = (uint8_t)kp;
         double *o = out + k * z->n_outputs;

@@ -40,7 +40,7 @@ class _Select(ctypes.Structure):
                 ("noise_scale", ctypes.c_double), ("pre_threshold", ctypes.c_int64),
                 ("max_rows_per_privacy_id", ctypes.c_int64),
                 ("pk_offset", ctypes.c_int64), ("public_mask", ctypes.c_void_p),
-                ("nonce", ctypes.c_uint64)]
+                ("nonce", ctypes.c_uint64), ("pk_stride", ctypes.c_int64)]
 
 
 class _Noise(ctypes.Structure):

@@ -20,7 +20,8 @@ EXPORTED = ("dpg_ctx_create", "dpg_ctx_destroy", "dpg_last_error", "dpg_set_seed
             "dpg_last_stage_times", "dpg_stream_seed", "dpg_preaggregate",
             "dpg_utility_analysis", "dpg_dataset_histograms",
             "dpg_comm_unique_id", "dpg_ctx_create_comm", "dpg_reduce_scatter_partials",
-            "dpg_pack_partials", "dpg_unpack_partials")
+            "dpg_pack_partials", "dpg_unpack_partials", "dpg_export_error",
+            "dpg_import_error")
 
 COMM_ID_BYTES = 128  # DPG_COMM_ID_BYTES
 
@@ -54,7 +55,7 @@ class SelectParams(ctypes.Structure):
                 ("noise_scale", ctypes.c_double), ("pre_threshold", ctypes.c_int64),
                 ("max_rows_per_privacy_id", ctypes.c_int64),
                 ("pk_offset", ctypes.c_int64), ("public_mask", ctypes.c_void_p),
-                ("nonce", ctypes.c_uint64)]
+                ("nonce", ctypes.c_uint64), ("pk_stride", ctypes.c_int64)]
 
 
 class NoiseParams(ctypes.Structure):
@@ -191,6 +192,10 @@ def load():
                                             ctypes.POINTER(ctypes.c_int64),
                                             ctypes.POINTER(ctypes.c_int64), vp]
         lib.dpg_unpack_partials.restype = ctypes.c_int
+        lib.dpg_export_error.argtypes = [vp, vp, vp]
+        lib.dpg_export_error.restype = ctypes.c_int
+        lib.dpg_import_error.argtypes = [vp, vp, i64, vp]
+        lib.dpg_import_error.restype = ctypes.c_int
         _lib = lib
         return lib
 
@@ -278,6 +283,15 @@ class Context:
                                           ctypes.byref(n), stream)
         self.check(st, "dpg_unpack_partials")
         return lo.value, n.value
+
+    def export_error(self, dst_ptr, stream):
+        """1.0 at device dst if the last bounding latched an internal error."""
+        self.check(self.lib.dpg_export_error(self.handle, dst_ptr, stream), "dpg_export_error")
+
+    def import_error(self, src_ptr, n: int, stream):
+        """Latches the internal error if any of n device doubles is nonzero
+        (the next compact then fails)."""
+        self.check(self.lib.dpg_import_error(self.handle, src_ptr, n, stream), "dpg_import_error")
 
     def select_and_noise(self, partials: Partials, sel: SelectParams, noise: NoiseParams,
                          keep_ptr, out_ptr, stream):

@@ -86,10 +86,11 @@ struct dpg_ctx {
     // read at the next synchronising call, dpg_compact_kept)
     const uint32_t *last_err = nullptr;
     int rank = 0, nranks = 1;
-    // pinned staging arena for host -> device uploads (see upload())
+    // pinned staging arena for host -> device uploads (see upload()): one
+    // completion event per stream that has uploaded through it
     char *stage_buf = nullptr;
     size_t stage_cap = 0, stage_head = 0;
-    hipEvent_t stage_done = nullptr;
+    std::map<hipStream_t, hipEvent_t> stage_done;
 };
 
 namespace {
@@ -173,16 +174,23 @@ void *ws(dpg_ctx *ctx, const char *name, size_t bytes, int *status) {
 // owned by the context and DMA'd from there, stream-ordered, so the source
 // may die as soon as this returns and the copy never stages pageable memory.
 // The arena is reused round-robin; when it wraps, the host waits for the
-// uploads already queued (rare: 4 MB, grown on demand).
+// uploads already queued on EVERY stream that has used it (rare: 4 MB, grown
+// on demand), so a copy still queued on another stream never reads bytes
+// that are being overwritten.
 int upload(dpg_ctx *ctx, void *dst, const void *src, size_t bytes, hipStream_t s) {
     if (bytes == 0) return DPG_OK;
     const size_t need = (bytes + 255) & ~(size_t)255;
-    if (!ctx->stage_done && hipEventCreateWithFlags(&ctx->stage_done, hipEventDisableTiming) != hipSuccess)
+    hipEvent_t &done = ctx->stage_done[s];
+    if (!done && hipEventCreateWithFlags(&done, hipEventDisableTiming) != hipSuccess) {
+        ctx->stage_done.erase(s);
         return fail(ctx, DPG_ERR_HIP, "hipEventCreate (upload arena)");
+    }
     if (need > ctx->stage_cap || ctx->stage_head + need > ctx->stage_cap) {
         // every queued upload must have left the arena before it is reused
-        if (ctx->stage_buf && hipEventSynchronize(ctx->stage_done) != hipSuccess)
-            return fail(ctx, DPG_ERR_HIP, "hipEventSynchronize (upload arena)");
+        if (ctx->stage_buf)
+            for (auto &kv : ctx->stage_done)
+                if (hipEventSynchronize(kv.second) != hipSuccess)
+                    return fail(ctx, DPG_ERR_HIP, "hipEventSynchronize (upload arena)");
         ctx->stage_head = 0;
         if (need > ctx->stage_cap) {
             if (ctx->stage_buf) (void)hipHostFree(ctx->stage_buf);
@@ -199,7 +207,7 @@ int upload(dpg_ctx *ctx, void *dst, const void *src, size_t bytes, hipStream_t s
     std::memcpy(p, src, bytes);
     ctx->stage_head += need;
     if (hipMemcpyAsync(dst, p, bytes, hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipEventRecord(ctx->stage_done, s) != hipSuccess)
+        hipEventRecord(done, s) != hipSuccess)
         return fail(ctx, DPG_ERR_HIP, "upload");
     return DPG_OK;
 }
@@ -1225,27 +1233,39 @@ std::string rccl_msg(ncclResult_t e) {
     return r.error_string ? std::string(r.error_string(e)) : "RCCL error " + std::to_string((int)e);
 }
 
-// Partials to the reduce-scatter layout [rank][array][S] (float64, zero
-// padded past P) and back (integer arrays are exact in float64 below 2^53).
+// Partials to the reduce-scatter layout and back.  Partition pk is owned by
+// rank pk mod R at local index pk / R (interleaved ownership: hot low ids,
+// e.g. an unpermuted Zipf key space, spread over every rank).  Rank r's block
+// is B = A * S + 1 doubles: [array][S] for its partitions, zero padded past
+// P, then the sender's internal-error flag, so that the sum over ranks
+// delivers every rank the flags of all of them.  Integer arrays are exact in
+// float64 below 2^53.
 struct PackArrays {
     const void *a[5];
     int is_int[5];
     int n;
 };
 
-__global__ void k_pack_partials(PackArrays src, int64_t P, int64_t S, int nranks, double *pack) {
+__global__ void k_pack_partials(PackArrays src, int64_t P, int64_t S, int nranks,
+                                const uint32_t *err, double *pack) {
+    const int64_t B = (int64_t)src.n * S + 1;
     const int64_t total = S * nranks;
+    // k enumerates partition ids: the reads are coalesced, each wave's
+    // stores form nranks runs
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < total;
          k += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t r = k / S, i = k - r * S;
+        const int64_t i = k / nranks, r = k - i * nranks;
         for (int j = 0; j < src.n; ++j) {
             double v = 0.0;
             if (k < P)
                 v = src.is_int[j] ? (double)static_cast<const int64_t *>(src.a[j])[k]
                                   : static_cast<const double *>(src.a[j])[k];
-            pack[(r * src.n + j) * S + i] = v;
+            pack[r * B + j * S + i] = v;
         }
     }
+    if (blockIdx.x == 0)
+        for (int r = threadIdx.x; r < nranks; r += blockDim.x)
+            pack[r * B + (int64_t)src.n * S] = (err && (*err & 2u)) ? 1.0 : 0.0;
 }
 
 struct UnpackArrays {
@@ -1254,8 +1274,12 @@ struct UnpackArrays {
     int n;
 };
 
+// part: this rank's summed block; latches a nonzero error sum into `err`
+// (the internal-error bit dpg_compact_kept checks)
 __global__ void k_unpack_partials(const double *part, int64_t S, int64_t n_local,
-                                  UnpackArrays dst) {
+                                  UnpackArrays dst, uint32_t *err) {
+    if (blockIdx.x == 0 && threadIdx.x == 0 && err && part[(int64_t)dst.n * S] != 0.0)
+        atomicOr(err, 2u);
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_local;
          i += (int64_t)gridDim.x * blockDim.x) {
         for (int j = 0; j < dst.n; ++j) {
@@ -1264,6 +1288,30 @@ __global__ void k_unpack_partials(const double *part, int64_t S, int64_t n_local
             else static_cast<double *>(dst.a[j])[i] = v;
         }
     }
+}
+
+__global__ void k_export_error(const uint32_t *err, double *dst) {
+    *dst = (err && (*err & 2u)) ? 1.0 : 0.0;
+}
+
+__global__ void k_import_error(const double *src, int64_t n, uint32_t *err) {
+    bool bad = false;
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) bad |= src[i] != 0.0;
+    if (bad) atomicOr(err, 2u);
+}
+
+// the word the next dpg_compact_kept checks: the last bounding's control
+// word, or (a context that has not bounded yet) a word of its own
+uint32_t *latch_word(dpg_ctx *ctx, hipStream_t s, int *status) {
+    if (ctx->last_err) return const_cast<uint32_t *>(ctx->last_err);
+    uint32_t *w = reinterpret_cast<uint32_t *>(ws(ctx, "comm.err", 4, status));
+    if (!w) return nullptr;
+    if (hipMemsetAsync(w, 0, 4, s) != hipSuccess) {
+        *status = fail(ctx, DPG_ERR_HIP, "hipMemsetAsync (error word)");
+        return nullptr;
+    }
+    ctx->last_err = w;
+    return w;
 }
 
 }  // namespace
@@ -1287,9 +1335,9 @@ void dpg_ctx_destroy(dpg_ctx *c) {
     for (auto &kv : c->bufs)
         if (kv.second.p) (void)hipFree(kv.second.p);
     for (auto e : c->events) (void)hipEventDestroy(e);
-    if (c->stage_done) {
-        (void)hipEventSynchronize(c->stage_done);
-        (void)hipEventDestroy(c->stage_done);
+    for (auto &kv : c->stage_done) {
+        (void)hipEventSynchronize(kv.second);
+        (void)hipEventDestroy(kv.second);
     }
     if (c->stage_buf) (void)hipHostFree(c->stage_buf);
     delete c;
@@ -1421,6 +1469,7 @@ int dpg_select_and_noise(dpg_ctx *ctx, const dpg_partials *in, const dpg_select_
     a.pre_threshold = sel->pre_threshold;
     a.max_rows = std::max<int64_t>(1, sel->max_rows_per_privacy_id);
     a.pk_offset = sel->pk_offset;
+    a.pk_stride = sel->pk_stride > 0 ? sel->pk_stride : 1;
     a.public_mask = sel->public_mask;
     a.table = nullptr;
     if (sel->strategy == DPG_SELECT_TRUNCATED_GEOMETRIC) {
@@ -1835,7 +1884,7 @@ int launch_pack(dpg_ctx *ctx, const PackArrays &pa, int64_t P, int R, double *pa
     const int64_t S = (P + R - 1) / R;
     const int64_t total = S * R;
     const unsigned blocks = (unsigned)std::min<int64_t>((total + 255) / 256, (int64_t)ctx->n_cu * 16);
-    k_pack_partials<<<blocks, 256, 0, s>>>(pa, P, S, R, pack);
+    k_pack_partials<<<blocks, 256, 0, s>>>(pa, P, S, R, ctx->last_err, pack);
     LAUNCH_CHECK();
     return st;
 }
@@ -1844,14 +1893,15 @@ int launch_unpack(dpg_ctx *ctx, const UnpackArrays &ua, const double *part, int6
                   int rank, dpg_partials *slice, int64_t *lo, int64_t *n, hipStream_t s) {
     int st = DPG_OK;
     const int64_t S = (P + R - 1) / R;
-    const int64_t l = std::min<int64_t>(P, (int64_t)rank * S);
-    const int64_t nl = std::min<int64_t>(P, l + S) - l;
-    if (nl > 0) {
-        const unsigned ub = (unsigned)std::min<int64_t>((nl + 255) / 256, (int64_t)ctx->n_cu * 16);
-        k_unpack_partials<<<ub, 256, 0, s>>>(part, S, nl, ua);
-        LAUNCH_CHECK();
-    }
-    *lo = l;
+    // partitions rank, rank + R, rank + 2R, ... below P
+    const int64_t nl = rank < P ? (P - rank + R - 1) / R : 0;
+    uint32_t *err = latch_word(ctx, s, &st);
+    if (!err) return st;
+    const unsigned ub = (unsigned)std::max<int64_t>(1, std::min<int64_t>((nl + 255) / 256,
+                                                                         (int64_t)ctx->n_cu * 16));
+    k_unpack_partials<<<ub, 256, 0, s>>>(part, S, nl, ua, err);
+    LAUNCH_CHECK();
+    *lo = rank;
     *n = nl;
     slice->n_partitions = nl;
     return st;
@@ -1900,13 +1950,37 @@ int dpg_reduce_scatter_partials(dpg_ctx *ctx, const dpg_partials *full, dpg_part
     PackArrays pa;
     UnpackArrays ua;
     if (int r = pack_arrays(ctx, full, slice, pa, ua)) return r;
-    WS(pack, double, "comm.pack", (size_t)R * pa.n * S);
-    WS(part, double, "comm.part", (size_t)pa.n * S);
+    WS(pack, double, "comm.pack", (size_t)R * (pa.n * S + 1));
+    WS(part, double, "comm.part", (size_t)pa.n * S + 1);
     if (int r = launch_pack(ctx, pa, P, R, pack, s)) return r;
-    const ncclResult_t e = rccl().reduce_scatter(pack, part, (size_t)pa.n * S, ncclFloat64, ncclSum,
+    const ncclResult_t e = rccl().reduce_scatter(pack, part, (size_t)pa.n * S + 1, ncclFloat64, ncclSum,
                                                  static_cast<ncclComm_t>(ctx->comm), s);
     if (e != ncclSuccess) return fail(ctx, DPG_ERR_HIP, "ncclReduceScatter: " + rccl_msg(e));
     return launch_unpack(ctx, ua, part, P, R, ctx->rank, slice, lo, n, s);
+}
+
+int dpg_export_error(dpg_ctx *ctx, double *dst, void *stream) {
+    if (!ctx || !dst) return DPG_ERR_INVALID_ARG;
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, DPG_ERR_HIP, "hipSetDevice");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    int st = DPG_OK;
+    k_export_error<<<1, 1, 0, s>>>(ctx->last_err, dst);
+    LAUNCH_CHECK();
+    return st;
+}
+
+int dpg_import_error(dpg_ctx *ctx, const double *src, int64_t n, void *stream) {
+    if (!ctx || !src || n < 0) return DPG_ERR_INVALID_ARG;
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, DPG_ERR_HIP, "hipSetDevice");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    int st = DPG_OK;
+    uint32_t *err = latch_word(ctx, s, &st);
+    if (!err) return st;
+    if (n > 0) {
+        k_import_error<<<1, 64, 0, s>>>(src, n, err);
+        LAUNCH_CHECK();
+    }
+    return st;
 }
 
 }  // extern "C"

@@ -111,7 +111,7 @@ struct SelectArgs {
     const double *table;  // device copy of the keep table (or null)
     double threshold, noise_scale;
     int64_t pre_threshold, max_rows;
-    int64_t pk_offset;
+    int64_t pk_offset, pk_stride;  // global pk of local partition k: pk_offset + k * pk_stride
     const uint8_t *public_mask;
 };
 
@@ -163,7 +163,7 @@ __global__ __launch_bounds__(256) void k_select_noise(const int64_t *rows, const
     const double *tab = lds_tab ? s_tab : s.table;
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < P;
          k += (int64_t)gridDim.x * blockDim.x) {
-        const uint64_t gk = (uint64_t)(k + s.pk_offset);
+        const uint64_t gk = (uint64_t)(s.pk_offset + k * s.pk_stride);
         const int64_t r = rows[k];
         const bool kp = keep_partition(s, seed, gk, k, r, tab);
         keep[k] = kp ? 1 : 0;

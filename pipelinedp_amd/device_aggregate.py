@@ -8,8 +8,9 @@ object keeps that contract: nothing touches the GPU until the first
 
 Device pipeline per call (include/dpg.h):
   dpg_bound_aggregate -> [multi-GPU: reduce-scatter of the dense partials,
-  or an all-to-all of the occupied ones: distributed.exchange_partials]
-  -> dpg_select_and_noise -> dpg_compact_kept.
+  or a fixed-block all-to-all of the occupied ones, with every rank's error
+  flag: distributed.exchange_partials] -> dpg_select_and_noise ->
+  dpg_compact_kept (the one host synchronisation after the bounding).
 """
 import ctypes
 import dataclasses
@@ -116,12 +117,13 @@ class DeviceAggregation:
                 f["mode"] = combiners.MODE_CROSS_AND_PER
         return f
 
-    def _select_fields(self, pk_offset: int, public_mask_local) -> dict:
+    def _select_fields(self, pk_offset: int, public_mask_local, pk_stride: int = 1) -> dict:
         nonce = self.nonce or 0
         if self.public_partitions is not None:
             return dict(strategy=0, table_len=0, keep_table=None, threshold=0.0,
                         noise_scale=0.0, pre_threshold=0, max_rows_per_privacy_id=1,
-                        pk_offset=pk_offset, public_mask=public_mask_local, nonce=nonce)
+                        pk_offset=pk_offset, pk_stride=pk_stride, public_mask=public_mask_local,
+                        nonce=nonce)
         spec = self.selection_spec
         sp = partition_selection.create_partition_selection_strategy(
             self.strategy, spec.eps, spec.delta, self.max_partitions_contributed,
@@ -131,26 +133,28 @@ class DeviceAggregation:
                  threshold=sp.threshold, noise_scale=sp.noise_scale,
                  pre_threshold=int(self.pre_threshold or 0),
                  max_rows_per_privacy_id=int(self.max_rows), pk_offset=pk_offset,
-                 public_mask=None, nonce=nonce)
+                 pk_stride=pk_stride, public_mask=None, nonce=nonce)
         if sp.table is not None:
             self._table = np.ascontiguousarray(np.asarray(sp.table, dtype=np.float64))
             f["table_len"] = len(self._table)
             f["keep_table"] = self._table.ctypes.data
         return f
 
-    def _release_nonce(self) -> int:
+    def _release_header(self, nnz_bound: int):
+        """The release nonce (rank 0's) and, with several ranks, the
+        occupancy bound maximised over ranks: one collective, before any
+        device work of the release."""
         if self.nonce is None:
             self.nonce = int.from_bytes(os.urandom(8), "little")
         if self.backend.world_size > 1:
-            self.nonce = distributed.broadcast_u64(self.nonce, self.backend.process_group,
-                                                   self.backend.device)
-        return self.nonce
+            self.nonce, nnz_bound = distributed.release_header(
+                self.nonce, nnz_bound, self.backend.process_group, self.backend.device)
+        return self.nonce, nnz_bound
 
     def _run(self, gather: bool) -> DeviceResult:
         backend = self.backend
         ctx = backend.ctx
         dev = backend.device
-        nonce = self._release_nonce()
         need_values = self.plan is not None and self.plan.needs_values()
         enc = columnar.encode(self.col, self.extractors, dev, need_values,
                               self.public_partitions,
@@ -170,6 +174,11 @@ class DeviceAggregation:
             raise ValueError(
                 "multi-GPU aggregation needs globally dense integer partition ids: "
                 "pass ColumnarData(..., n_partitions=P) with pk in [0, P) on every rank")
+        bfields = self._bound_fields(P)
+        l0 = (bfields["max_contributions"] if bfields["mode"] == combiners.MODE_PER_PID
+              else bfields["max_partitions_contributed"])
+        nonce, nnz_bound = self._release_header(distributed.occupancy_bound(
+            P, enc.n, enc.pid_count, int(l0)))
         with torch.cuda.device(dev):
             stream = torch.cuda.current_stream(dev)
             sptr = ctypes.c_void_p(stream.cuda_stream)
@@ -181,7 +190,6 @@ class DeviceAggregation:
             var = mask & (combiners.M_MEAN | combiners.M_VARIANCE)
             nsum = torch.empty(P, **f64) if var else None
             nsq = torch.empty(P, **f64) if var else None
-            bfields = self._bound_fields(P)
             bound = _native.fill(_native.BoundParams, bfields)
             bound.pid_min, bound.pid_count = enc.pid_min, enc.pid_count
             bound.rec_id_offset = enc.rec_id_offset
@@ -204,23 +212,30 @@ class DeviceAggregation:
             stage_ms = {}
             tensors = dict(rows=rows, count=count, sum=sum_, nsum=nsum, nsq=nsq)
             self.last_partials = tensors
-            pk_offset, local_P = 0, P
+            pk_offset, pk_stride, local_P = 0, 1, P
             public_mask_local = enc.public_mask
             self.last_exchange = None
             if backend.world_size > 1:
-                tensors, pk_offset, local_P, self.last_exchange = distributed.exchange_partials(
-                    tensors, P, backend.process_group, backend.exchange)
+                err = torch.empty(1, **f64)
+                ctx.export_error(err.data_ptr(), sptr)
+                tensors, (pk_offset, pk_stride, local_P), self.last_exchange, flags = \
+                    distributed.exchange_partials(tensors, P, backend.process_group,
+                                                  backend.exchange, nnz_bound, err)
+                # any rank's bounding error fails this rank's compaction
+                flags = flags.to(dev).contiguous()
+                ctx.import_error(flags.data_ptr(), flags.numel(), sptr)
                 if public_mask_local is not None:
                     public_mask_local = distributed.slice_bitmap(
-                        enc.public_mask, pk_offset, local_P)
-            # this rank's merged slice [pk_offset, pk_offset + local_P)
-            self.last_slice = (tensors, pk_offset, local_P)
+                        enc.public_mask, pk_offset, pk_stride, local_P)
+            # this rank's merged partitions pk_offset + i * pk_stride, i < local_P
+            self.last_slice = (tensors, pk_offset, pk_stride, local_P)
             lp = _native.Partials(local_P, tensors["rows"].data_ptr(),
                                   tensors["count"].data_ptr(),
                                   *(tensors[k].data_ptr() if tensors[k] is not None else None
                                     for k in ("sum", "nsum", "nsq")))
             sfields = self._select_fields(
-                pk_offset, public_mask_local.data_ptr() if public_mask_local is not None else None)
+                pk_offset, public_mask_local.data_ptr() if public_mask_local is not None else None,
+                pk_stride)
             self.last_select_fields = sfields
             sel = _native.fill(_native.SelectParams, sfields)
             nz = _native.fill(_native.NoiseParams, noise)
@@ -232,7 +247,7 @@ class DeviceAggregation:
             kept_out = torch.empty(max(local_P * n_out, 1), **f64)
             k = ctx.compact(keep.data_ptr(), out.data_ptr(), local_P, n_out, ids.data_ptr(),
                             kept_out.data_ptr(), sptr)
-            ids = ids[:k] + pk_offset
+            ids = ids[:k] * pk_stride + pk_offset
             vals = kept_out[:k * n_out].view(k, n_out) if n_out else torch.empty((k, 0), **f64)
             if backend.world_size > 1 and gather:
                 ids, vals = distributed.all_gather_results(ids, vals, backend.process_group)

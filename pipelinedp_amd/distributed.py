@@ -2,31 +2,44 @@
 
 Records are sharded by privacy id before they reach a rank (each privacy id
 lives on exactly one GPU), so contribution bounding is shard-local and the
-only exchange is the merge of the per-partition partials.  Every rank owns
-an equal, contiguous slice of the partition space; the owner runs
-selection + noise for its slice, and the kept results are all-gathered.
-Two exchanges reach that slice:
+only exchange is the merge of the per-partition partials.
+
+Ownership is by partition key: rank r owns partitions r, r + R, r + 2R, ...
+(R ranks; `pk mod R`, the identity hash of the dense ids), at local index
+pk // R.  Interleaving spreads hot low ids -- an unpermuted Zipf key space
+puts most of its occupied partitions at the bottom -- over every rank, so the
+sparse exchange's receive volume and every rank's selection work stay
+balanced whatever the key order.  The owner runs selection + noise for its
+partitions and the kept results are all-gathered (SURVEY.md 8(e);
+DESIGN.md section 5).  Two exchanges reach the owner:
 
 * dense -- ONE `reduce_scatter` (sum) of all accumulator arrays packed
-  together: 8 B x P x A per rank (A = accumulator arrays; P = 1e6,
-  COUNT+SUM+PID: 24 MB), whatever the occupancy;
-* sparse -- ONE `all_to_all` of the occupied partitions only, as rows
-  (pk, partial_1..A) routed to the rank owning pk: 8 B x (1 + A) x nnz per
-  rank (nnz = partitions with a kept pair on that rank), after a
-  world-sized count exchange.  Config 4 (P = 1e8, ~1e7 occupied) moves
-  ~0.5 GB instead of 4 GB per rank.
+  together: 8 B x (A x S + 1) per destination, S = ceil(P / R) (A =
+  accumulator arrays; P = 1e6, COUNT+SUM+PID: 24 MB per rank), whatever
+  the occupancy;
+* sparse -- ONE `all_to_all` with equal splits: every destination gets a
+  fixed block of `cap` rows (pk, partial_1..A) (padding rows pk = -1), cap =
+  min(S, an upper bound on the partitions one rank can occupy), so no count
+  exchange and no host round trip of split sizes is needed.
 
-`exchange_partials` picks the cheaper one from the largest nnz over ranks
-(one all_reduce of a scalar, so every rank takes the same branch).  The
-integer accumulators travel as float64, which is exact below 2^53 (a rank
-holds < 2^32 records, so no count comes near it).  With gloo (CPU tests,
-and several ranks sharing one GPU) the collectives are staged through host
-memory and the reduce-scatter is an all_reduce + slice.
+Neither exchange synchronises the host: the choice between them is made
+from host-known sizes only (`choose_exchange`: P, A, R and the occupancy
+bound min(P, records, privacy ids x l0), maximised over ranks in the one
+collective that already carries the release nonce, `release_header`), and
+the split sizes are static.  Every block also carries its sender's
+internal-error flag (a bounding whose table overflowed); the owner latches
+the sum (`dpg_import_error`), so an error on any rank fails every rank's
+`dpg_compact_kept` instead of releasing partials of a mis-bounded shard.
+
+The integer accumulators travel as float64, exact below 2^53 (a rank holds
+< 2^32 records).  With gloo (CPU tests, and several ranks sharing one GPU)
+the collectives are staged through host memory and the reduce-scatter is an
+all_reduce + slice.
 
 Every random draw is keyed by (stream seed, pid, pk) or (stream seed, pk)
-with global partition ids -- never by rank -- and the release nonce is
-broadcast from rank 0, so the selected-partition set is identical for any
-world size.
+with global partition ids -- never by rank -- and the release nonce comes
+from rank 0, so the selected-partition set is identical for any world size
+(SURVEY.md 8(e)).
 """
 from typing import Dict, Optional, Tuple
 
@@ -34,6 +47,7 @@ import torch
 import torch.distributed as dist
 
 _PACK_ORDER = ("rows", "count", "sum", "nsum", "nsq")
+_I64_MIN = -(1 << 63)
 
 
 def shard_of(pid: torch.Tensor, world_size: int) -> torch.Tensor:
@@ -43,153 +57,203 @@ def shard_of(pid: torch.Tensor, world_size: int) -> torch.Tensor:
     return ((h * world_size) >> 32).to(torch.int64)
 
 
-def slice_bounds(P: int, world_size: int, rank: int) -> Tuple[int, int]:
-    chunk = (P + world_size - 1) // world_size
-    lo = min(P, rank * chunk)
-    return lo, min(P, lo + chunk) - lo
+def owned(P: int, world_size: int, rank: int) -> Tuple[int, int, int]:
+    """(lo, stride, n): this rank owns partitions lo + i * stride, i < n."""
+    n = (P - rank + world_size - 1) // world_size if rank < P else 0
+    return rank, world_size, n
+
+
+def owner_of(pk: torch.Tensor, world_size: int) -> torch.Tensor:
+    return pk.to(torch.int64) % world_size
 
 
 def _is_nccl(group) -> bool:
     return dist.get_backend(group) == "nccl"
 
 
+def _coll_device(group, device):
+    return device if _is_nccl(group) else torch.device("cpu")
+
+
 def broadcast_u64(x: int, group, device) -> int:
-    """Rank 0's 64-bit value on every rank (the release nonce)."""
-    signed = x - (1 << 64) if x >= (1 << 63) else x
-    dev = device if _is_nccl(group) else torch.device("cpu")
-    t = torch.tensor([signed], dtype=torch.int64, device=dev)
-    dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None else 0,
-                   group=group)
-    return int(t.item()) & ((1 << 64) - 1)
+    """Rank 0's 64-bit value on every rank."""
+    return release_header(x, 0, group, device)[0]
 
 
-def reduce_scatter_partials(tensors: Dict[str, Optional[torch.Tensor]], P: int, group
-                            ) -> Tuple[Dict[str, Optional[torch.Tensor]], int, int]:
-    """Sums the dense partials over ranks and returns this rank's slice
-    [lo, lo + n) of every array, with one collective for all of them."""
-    world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
-    chunk = (P + world - 1) // world
-    padded = chunk * world
-    lo, n_local = slice_bounds(P, world, rank)
-    names = [k for k in _PACK_ORDER if tensors.get(k) is not None]
-    like = tensors[names[0]]
-    dev = like.device
-    # layout [world][array][chunk]: rank r's reduce-scatter block is the
-    # contiguous [array][chunk] slab of its partition slice
-    pack = torch.zeros((len(names), padded), dtype=torch.float64, device=dev)
-    for j, k in enumerate(names):
-        pack[j, :P] = tensors[k].to(torch.float64)
-    pack = pack.view(len(names), world, chunk).transpose(0, 1).contiguous()
-    if _is_nccl(group):
-        part = torch.empty((len(names), chunk), dtype=torch.float64, device=dev)
-        dist.reduce_scatter_tensor(part, pack, op=dist.ReduceOp.SUM, group=group)
-    else:
-        host = pack.cpu()
-        dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
-        part = host[rank].to(dev)
-    out: Dict[str, Optional[torch.Tensor]] = {k: None for k in _PACK_ORDER}
-    for j, k in enumerate(names):
-        col = part[j, :n_local]
-        out[k] = (col.round().to(torch.int64) if tensors[k].dtype == torch.int64
-                  else col).contiguous()
-    return out, lo, n_local
+def release_header(nonce: int, nnz_bound: int, group, device) -> Tuple[int, int]:
+    """ONE all_reduce (max) before a release: rank 0's nonce (the others
+    contribute INT64_MIN) and the largest occupancy bound over ranks, so
+    every rank draws the same streams and takes the same exchange."""
+    signed = nonce - (1 << 64) if nonce >= (1 << 63) else nonce
+    root = dist.get_global_rank(group, 0) if group is not None else 0
+    mine = signed if dist.get_rank() == root else _I64_MIN
+    t = torch.tensor([mine, int(nnz_bound)], dtype=torch.int64,
+                     device=_coll_device(group, device))
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    got = t.tolist()
+    return got[0] & ((1 << 64) - 1), got[1]
 
 
 def _names(tensors) -> list:
     return [k for k in _PACK_ORDER if tensors.get(k) is not None]
 
 
-def exchange_bytes(P: int, nnz: int, n_arrays: int) -> Dict[str, int]:
-    """Bytes one rank contributes to each exchange (the send side)."""
-    return {"reduce_scatter": 8 * n_arrays * P, "all_to_all": 8 * (1 + n_arrays) * nnz}
+def _interleaved(t: torch.Tensor, P: int, world: int, S: int) -> torch.Tensor:
+    """[world, S] float64 view of partition array t: element (r, i) is
+    partition i * world + r (zero past P)."""
+    x = torch.zeros(S * world, dtype=torch.float64, device=t.device)
+    x[:P] = t.to(torch.float64)
+    return x.view(S, world).t()
 
 
-def choose_exchange(rows: torch.Tensor, P: int, n_arrays: int, group, mode: str = "auto"
-                    ) -> Tuple[str, int]:
-    """The exchange every rank of `group` uses, and the largest occupancy
-    over ranks.  'auto' takes the sparse all-to-all when its rows are at
-    most half the dense reduce-scatter's bytes (the count exchange and the
-    host round trip for the split sizes cost latency the dense path does
-    not pay)."""
-    if mode not in ("auto", "reduce_scatter", "all_to_all"):
-        raise ValueError(f"unknown exchange {mode!r}")
-    nnz = int(torch.count_nonzero(rows).item())
-    dev = rows.device if _is_nccl(group) else torch.device("cpu")
-    t = torch.tensor([nnz], dtype=torch.int64, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
-    nnz_max = int(t.item())
-    if mode != "auto":
-        return mode, nnz_max
-    b = exchange_bytes(P, nnz_max, n_arrays)
-    return ("all_to_all" if 2 * b["all_to_all"] <= b["reduce_scatter"] else "reduce_scatter",
-            nnz_max)
+def _unpack_column(col: torch.Tensor, like: torch.Tensor) -> torch.Tensor:
+    return (col.round().to(torch.int64) if like.dtype == torch.int64 else col).contiguous()
 
 
-def all_to_all_partials(tensors: Dict[str, Optional[torch.Tensor]], P: int, group
-                        ) -> Tuple[Dict[str, Optional[torch.Tensor]], int, int]:
-    """Sparse merge: the occupied partitions (rows > 0) of every rank travel
-    as (pk, partials...) rows to the rank owning pk's slice; the owner adds
-    them into its dense slice, source rank by source rank (pks are unique
-    within one source, so every add is conflict-free and the merge is
-    deterministic).  Same result as reduce_scatter_partials."""
+def reduce_scatter_partials(tensors: Dict[str, Optional[torch.Tensor]], P: int, group,
+                            err: Optional[torch.Tensor] = None):
+    """Sums the dense partials over ranks; returns this rank's partitions
+    of every array, (lo, stride, n) and the summed error flags (a [1]
+    float64 tensor on the partials' device), with one collective for all
+    of them.  Layout [rank][array][S] + one error slot per rank block --
+    the C ABI's dpg_pack_partials layout."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    chunk = (P + world - 1) // world
-    lo, n_local = slice_bounds(P, world, rank)
+    S = (P + world - 1) // world
+    lo, stride, n_local = owned(P, world, rank)
     names = _names(tensors)
+    A = len(names)
     dev = tensors[names[0]].device
-    nccl = _is_nccl(group)
-    cdev = dev if nccl else torch.device("cpu")
-    idx = torch.nonzero(tensors["rows"]).flatten()  # ascending, so grouped by owner
-    send = torch.empty((idx.numel(), 1 + len(names)), dtype=torch.float64, device=dev)
-    send[:, 0] = idx.to(torch.float64)
+    pack = torch.empty((world, A * S + 1), dtype=torch.float64, device=dev)
     for j, k in enumerate(names):
-        send[:, 1 + j] = tensors[k][idx].to(torch.float64)
-    send_counts = torch.bincount(idx // chunk, minlength=world).to(torch.int64)
-    recv_counts = torch.empty_like(send_counts, device=cdev)
-    dist.all_to_all_single(recv_counts, send_counts.to(cdev), group=group)
-    sc, rc = send_counts.tolist(), recv_counts.tolist()
-    recv = torch.empty((sum(rc), 1 + len(names)), dtype=torch.float64, device=cdev)
-    dist.all_to_all_single(recv, send.to(cdev), output_split_sizes=rc, input_split_sizes=sc,
-                           group=group)
-    recv = recv.to(dev)
-    acc = torch.zeros((len(names), n_local), dtype=torch.float64, device=dev)
-    o = 0
-    for c in rc:  # source rank order
-        if c:
-            blk = recv[o:o + c]
-            li = blk[:, 0].round().to(torch.int64) - lo
-            acc[:, li] += blk[:, 1:].t()
-        o += c
+        pack[:, j * S:(j + 1) * S] = _interleaved(tensors[k], P, world, S)
+    pack[:, A * S] = err.to(dev).reshape(()) if err is not None else 0.0
+    if _is_nccl(group):
+        part = torch.empty(A * S + 1, dtype=torch.float64, device=dev)
+        dist.reduce_scatter_tensor(part, pack.view(-1), op=dist.ReduceOp.SUM, group=group)
+    else:
+        host = pack.cpu()
+        dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
+        part = host[rank].to(dev)
     out: Dict[str, Optional[torch.Tensor]] = {k: None for k in _PACK_ORDER}
     for j, k in enumerate(names):
-        col = acc[j]
-        out[k] = (col.round().to(torch.int64) if tensors[k].dtype == torch.int64
-                  else col).contiguous()
-    return out, lo, n_local
+        out[k] = _unpack_column(part[j * S:j * S + n_local], tensors[k])
+    return out, (lo, stride, n_local), part[A * S:A * S + 1]
+
+
+def occupancy_bound(P: int, n_records: int, pid_count: int, l0: int) -> int:
+    """Upper bound on the partitions one rank's kept pairs can reach: at
+    most one per record, at most l0 per privacy id, at most P."""
+    b = min(P, max(0, n_records))
+    if pid_count > 0 and l0 > 0:
+        b = min(b, pid_count * l0)
+    return max(1, b)
+
+
+def exchange_bytes(P: int, nnz_bound: int, n_arrays: int, world: int = 1) -> Dict[str, int]:
+    """Bytes one rank sends in each exchange."""
+    S = (P + world - 1) // world
+    cap = min(S, nnz_bound)
+    return {"reduce_scatter": 8 * world * (n_arrays * S + 1),
+            "all_to_all": 8 * world * (cap + 1) * (1 + n_arrays)}
+
+
+def choose_exchange(P: int, n_arrays: int, world: int, nnz_bound: int, mode: str = "auto") -> str:
+    """The exchange of one release, from sizes every rank agrees on (no
+    device data): 'auto' takes the sparse all-to-all when its fixed blocks
+    are at most half the dense reduce-scatter's bytes."""
+    if mode not in ("auto", "reduce_scatter", "all_to_all"):
+        raise ValueError(f"unknown exchange {mode!r}")
+    if mode != "auto":
+        return mode
+    b = exchange_bytes(P, nnz_bound, n_arrays, world)
+    return "all_to_all" if 2 * b["all_to_all"] <= b["reduce_scatter"] else "reduce_scatter"
+
+
+def all_to_all_partials(tensors: Dict[str, Optional[torch.Tensor]], P: int, group,
+                        nnz_bound: int, err: Optional[torch.Tensor] = None):
+    """Sparse merge: the occupied partitions (rows > 0) of every rank travel
+    as (pk, partials...) rows to their owner in fixed blocks of cap rows per
+    destination (equal splits: nothing about the occupancy reaches the
+    host).  The owner adds them into its dense slice source rank by source
+    rank (pks are unique within one source, so every add is conflict-free
+    and the merge is deterministic).  Same result as
+    reduce_scatter_partials.  A block with more occupied partitions than cap
+    (impossible when nnz_bound bounds the occupancy) raises the error flag."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    S = (P + world - 1) // world
+    cap = max(1, min(S, int(nnz_bound)))
+    lo, stride, n_local = owned(P, world, rank)
+    names = _names(tensors)
+    A = len(names)
+    dev = tensors[names[0]].device
+    occ = _interleaved(tensors["rows"], P, world, S) > 0          # [world, S]
+    pos = occ.to(torch.int64).cumsum(1) - 1
+    fits = occ & (pos < cap)
+    over = (occ & ~fits).any().to(torch.float64)
+    blk = cap + 1                                                  # header row + cap rows
+    sink = world * blk                                             # rows past the cap, padding
+    dst = torch.where(fits, torch.arange(world, device=dev).view(-1, 1) * blk + 1 + pos,
+                      torch.full_like(pos, sink))
+    grid = (torch.arange(S, device=dev).view(1, -1) * world +
+            torch.arange(world, device=dev).view(-1, 1)).to(torch.float64)
+    rows = torch.stack([grid] + [_interleaved(tensors[k], P, world, S) for k in names], -1)
+    send = torch.zeros((sink + 1, 1 + A), dtype=torch.float64, device=dev)
+    send[:, 0] = -1.0
+    send.index_copy_(0, dst.reshape(-1), rows.reshape(-1, 1 + A))
+    hdr = torch.arange(world, device=dev) * blk
+    send[hdr, 0] = -2.0
+    send[hdr, 1] = (err.to(dev).reshape(()) if err is not None else 0.0) + over
+    send = send[:sink].contiguous()
+    nccl = _is_nccl(group)
+    if nccl:
+        recv = torch.empty_like(send)
+        dist.all_to_all_single(recv, send, group=group)
+    else:
+        recv = torch.empty_like(send, device="cpu")
+        dist.all_to_all_single(recv, send.cpu(), group=group)
+        recv = recv.to(dev)
+    recv = recv.view(world, blk, 1 + A)
+    flags = recv[:, 0, 1].sum().reshape(1)
+    acc = torch.zeros((A, n_local + 1), dtype=torch.float64, device=dev)
+    for src in range(world):  # source rank order: deterministic sums
+        body = recv[src, 1:]
+        pk = body[:, 0]
+        li = torch.where(pk >= 0, (pk.round().to(torch.int64) - lo) // stride,
+                         torch.full_like(pk, n_local, dtype=torch.int64))
+        acc.index_add_(1, li, body[:, 1:].t().contiguous())
+    out: Dict[str, Optional[torch.Tensor]] = {k: None for k in _PACK_ORDER}
+    for j, k in enumerate(names):
+        out[k] = _unpack_column(acc[j, :n_local], tensors[k])
+    return out, (lo, stride, n_local), flags
 
 
 def exchange_partials(tensors: Dict[str, Optional[torch.Tensor]], P: int, group,
-                      mode: str = "auto"):
-    """Merges the partials of every rank into this rank's slice with the
-    exchange `choose_exchange` picks.  Returns (slice tensors, lo, n,
-    info) where info names the exchange and its per-rank send bytes."""
+                      mode: str = "auto", nnz_bound: Optional[int] = None,
+                      err: Optional[torch.Tensor] = None):
+    """Merges the partials of every rank into this rank's partitions with
+    the exchange `choose_exchange` picks.  nnz_bound must be the same on
+    every rank (release_header); None = P.  Returns (tensors, (lo, stride,
+    n), info, error flags) where info names the exchange and its per-rank
+    send bytes."""
     names = _names(tensors)
-    chosen, nnz_max = choose_exchange(tensors["rows"], P, len(names), group, mode)
+    world = dist.get_world_size(group)
+    bound = P if nnz_bound is None else int(nnz_bound)
+    chosen = choose_exchange(P, len(names), world, bound, mode)
     if chosen == "all_to_all":
-        out, lo, n = all_to_all_partials(tensors, P, group)
+        out, own, flags = all_to_all_partials(tensors, P, group, bound, err)
     else:
-        out, lo, n = reduce_scatter_partials(tensors, P, group)
-    info = {"mode": chosen, "backend": dist.get_backend(group),
-            "world_size": dist.get_world_size(group), "nnz_max": nnz_max,
-            "send_bytes": exchange_bytes(P, nnz_max, len(names))[chosen]}
-    return out, lo, n, info
+        out, own, flags = reduce_scatter_partials(tensors, P, group, err)
+    info = {"mode": chosen, "backend": dist.get_backend(group), "world_size": world,
+            "nnz_bound": bound,
+            "send_bytes": exchange_bytes(P, bound, len(names), world)[chosen]}
+    return out, own, info, flags
 
 
-def slice_bitmap(mask: torch.Tensor, lo: int, n: int) -> torch.Tensor:
-    """Bitmap of partitions [lo, lo + n) re-based to bit 0."""
-    ids = torch.arange(lo, lo + n, device=mask.device)
+def slice_bitmap(mask: torch.Tensor, lo: int, stride: int, n: int) -> torch.Tensor:
+    """Bitmap of partitions lo + i * stride (i < n) re-based to bit i."""
+    ids = lo + torch.arange(n, device=mask.device) * stride
     bits = ((mask[ids >> 3].to(torch.int64) >> (ids & 7)) & 1).to(torch.uint8)
     padded = torch.zeros(((n + 7) // 8) * 8, dtype=torch.uint8, device=mask.device)
     padded[:n] = bits
@@ -200,11 +264,11 @@ def slice_bitmap(mask: torch.Tensor, lo: int, n: int) -> torch.Tensor:
 def all_gather_results(ids: torch.Tensor, vals: torch.Tensor, group):
     """Concatenates every rank's kept (ids, values) in rank order: one size
     exchange, then one all_gather of ids and values packed as float64 rows
-    (ids < 2^32 are exact)."""
+    (ids < 2^53 are exact).  Runs after dpg_compact_kept, which has already
+    synchronised the host."""
     world = dist.get_world_size(group)
-    nccl = _is_nccl(group)
     dev = ids.device
-    cdev = dev if nccl else torch.device("cpu")
+    cdev = _coll_device(group, dev)
     n = torch.tensor([ids.numel()], dtype=torch.int64, device=cdev)
     sizes = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(sizes, n, group=group)

@@ -214,8 +214,11 @@ class MI355XBackend(_HostCollectionOps, PipelineBackend):
       process_group: torch.distributed group for multi-GPU aggregation
         (records must be sharded by privacy id); None = single GPU.
       exchange: how the ranks merge their per-partition partials
-        (distributed.py): 'auto' (by occupancy), 'reduce_scatter' (dense)
-        or 'all_to_all' (sparse rows of the occupied partitions).
+        (distributed.py): 'auto' (from P, the accumulator arrays and the
+        occupancy bound min(P, records, privacy ids x l0) -- no device
+        data, no host synchronisation), 'reduce_scatter' (dense) or
+        'all_to_all' (fixed blocks of the occupied partitions' rows).
+        Partition pk is owned by rank pk mod world_size.
     """
 
     def __init__(self, device: Optional[int] = None, seed: Optional[int] = None,

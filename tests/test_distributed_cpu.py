@@ -33,7 +33,7 @@ FIELDS = dict(mode=0, sum_mode=1, metric_mask=7, max_partitions_contributed=3,
               n_partitions=P)
 
 
-def _worker(rank, world, port, q, mode):
+def _worker(rank, world, port, q, mode, bad_rank):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     pid, pk, val = _data()
@@ -43,19 +43,22 @@ def _worker(rank, world, port, q, mode):
     part = oracle.bound_aggregate(pid[m], pk[m], val[m], FIELDS, 99, rec_ids=np.nonzero(m)[0])
     tens = {k: torch.as_tensor(part[k]) for k in ("rows", "count", "sum")}
     tens.update(nsum=None, nsq=None)
-    if mode == "reduce_scatter":
-        out, lo, n = distributed.reduce_scatter_partials(tens, P, dist.group.WORLD)
-    else:
-        out, lo, n, info = distributed.exchange_partials(tens, P, dist.group.WORLD, mode)
-        assert info["mode"] == "all_to_all" and info["world_size"] == world
-    # kept results: partitions of this slice with rows > 0, values = counts
-    ids = torch.nonzero(out["rows"] > 0).flatten() + lo
-    vals = out["count"][ids - lo].to(torch.float64).view(-1, 1)
+    # one rank may report a latched bounding error: every rank must see it
+    err = torch.tensor([1.0 if rank == bad_rank else 0.0], dtype=torch.float64)
+    nonce, bound = distributed.release_header(0xFEED0000 + rank, int(m.sum()), dist.group.WORLD,
+                                              torch.device("cpu"))
+    out, (lo, stride, n), info, flags = distributed.exchange_partials(
+        tens, P, dist.group.WORLD, mode, bound, err)
+    assert info["mode"] == mode and info["world_size"] == world
+    # kept results: partitions of this rank with rows > 0, values = counts
+    li = torch.nonzero(out["rows"] > 0).flatten()
+    ids = li * stride + lo
+    vals = out["count"][li].to(torch.float64).view(-1, 1)
     g_ids, g_vals = distributed.all_gather_results(ids, vals, dist.group.WORLD)
     bm = torch.as_tensor(oracle.bitmap(np.arange(0, P, 3), P))
-    sl = distributed.slice_bitmap(bm, lo, n)
-    q.put((rank, lo, n, {k: v.numpy() for k, v in out.items() if v is not None},
-           g_ids.numpy(), g_vals.numpy(), sl.numpy()))
+    sl = distributed.slice_bitmap(bm, lo, stride, n)
+    q.put((rank, lo, stride, n, {k: v.numpy() for k, v in out.items() if v is not None},
+           g_ids.numpy(), g_vals.numpy(), sl.numpy(), float(flags.sum()), nonce, bound))
     dist.destroy_process_group()
 
 
@@ -67,67 +70,93 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world,mode", [(2, "reduce_scatter"), (2, "all_to_all"),
-                                        (3, "all_to_all")])
-def test_rank_merge_equals_single_process(world, mode):
+def _run(world, target, *args):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, mode)) for r in range(world)]
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    return res
+
+
+@pytest.mark.parametrize("world,mode,bad", [(2, "reduce_scatter", -1), (2, "all_to_all", -1),
+                                            (3, "all_to_all", 1), (3, "reduce_scatter", 2)])
+def test_rank_merge_equals_single_process(world, mode, bad):
+    res = _run(world, _worker, mode, bad)
     pid, pk, val = _data()
     ref = oracle.bound_aggregate(pid, pk, val, FIELDS, 99)
-    for rank, lo, n, out, g_ids, g_vals, sl in res:
-        assert np.array_equal(out["rows"], ref["rows"][lo:lo + n])
-        assert np.array_equal(out["count"], ref["count"][lo:lo + n])
-        assert np.allclose(out["sum"], ref["sum"][lo:lo + n], rtol=1e-12)
+    every = np.arange(0, P, 3)
+    n_rec = [int((distributed.shard_of(torch.as_tensor(pid), world).numpy() == r).sum())
+             for r in range(world)]
+    for rank, lo, stride, n, out, g_ids, g_vals, sl, flags, nonce, bound in res:
+        own = lo + stride * np.arange(n)          # interleaved ownership: pk mod world
+        assert lo == rank and stride == world and np.array_equal(own, np.arange(rank, P, world))
+        assert np.array_equal(out["rows"], ref["rows"][own])
+        assert np.array_equal(out["count"], ref["count"][own])
+        assert np.allclose(out["sum"], ref["sum"][own], rtol=1e-12)
         want_ids = np.nonzero(ref["rows"] > 0)[0]
         assert np.array_equal(np.sort(g_ids), want_ids)
         bits = np.unpackbits(sl, bitorder="little")[:n]
-        assert np.array_equal(np.nonzero(bits)[0] + lo, np.arange(0, P, 3)[(np.arange(0, P, 3) >= lo) & (np.arange(0, P, 3) < lo + n)])
-    chunk = (P + world - 1) // world
-    assert sorted(r[1] for r in res) == [r * chunk for r in range(world)]
+        assert np.array_equal(own[np.nonzero(bits)[0]], every[every % world == rank])
+        # every rank sees the error of any rank, and rank 0's nonce
+        assert flags == (1.0 if bad >= 0 else 0.0)
+        assert nonce == 0xFEED0000 and bound == max(n_rec)
 
 
-def _choose_worker(rank, world, port, q):
+def _hot_worker(rank, world, port, q):
+    """Unpermuted Zipf keys: the hot partitions are the lowest ids."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    Pbig = 1_000_000
-    rows = torch.zeros(Pbig, dtype=torch.int64)
-    # rank 1 is the fuller one: the choice must follow the largest occupancy
-    nnz = 1000 if rank == 0 else (50_000 if q is not None and world == 2 else 1000)
-    rows[torch.arange(nnz) * 7] = 1
-    sparse = distributed.choose_exchange(rows, Pbig, 3, dist.group.WORLD)
-    rows[:] = 1
-    dense = distributed.choose_exchange(rows, Pbig, 3, dist.group.WORLD)
-    forced = distributed.choose_exchange(rows, Pbig, 3, dist.group.WORLD, "all_to_all")
-    q.put((rank, sparse, dense, forced))
+    Pbig = 100_000
+    rng = np.random.default_rng(rank)
+    pk = np.minimum(rng.zipf(1.3, 50_000) - 1, Pbig - 1)
+    rows = torch.as_tensor(np.bincount(pk, minlength=Pbig).astype(np.int64))
+    tens = dict(rows=rows, count=rows.clone(), sum=rows.to(torch.float64), nsum=None, nsq=None)
+    out, (lo, stride, n), info, _ = distributed.exchange_partials(
+        tens, Pbig, dist.group.WORLD, "all_to_all", 50_000)
+    q.put((rank, int((out["rows"] > 0).sum()), int(out["rows"].sum())))
     dist.destroy_process_group()
 
 
-def test_exchange_choice_is_global_and_by_occupancy():
-    world = 2
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_choose_worker, args=(r, world, port, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = [q.get(timeout=120) for _ in range(world)]
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    for rank, sparse, dense, forced in res:
-        assert sparse == ("all_to_all", 50_000)   # max over ranks, same on both
-        assert dense == ("reduce_scatter", 1_000_000)
-        assert forced == ("all_to_all", 1_000_000)
-    b = distributed.exchange_bytes(100_000_000, 10_000_000, 5)
-    assert b["all_to_all"] * 6 < b["reduce_scatter"]
+def test_interleaved_owners_balance_hot_low_ids():
+    """ADVICE/VERDICT r3: contiguous slices put an unpermuted Zipf key
+    space's occupied partitions on rank 0; pk mod R ownership splits both
+    the occupied partitions and the rows evenly."""
+    world = 4
+    res = _run(world, _hot_worker)
+    occ = np.array([r[1] for r in sorted(res)])
+    rows = np.array([r[2] for r in sorted(res)])
+    assert occ.min() > 0.8 * occ.max(), occ
+    assert rows.sum() == world * 50_000
+    # contiguous slices for comparison: the first quarter holds nearly all
+    pk = np.concatenate([np.minimum(np.random.default_rng(r).zipf(1.3, 50_000) - 1, 99_999)
+                         for r in range(world)])
+    contiguous = np.bincount(np.unique(pk) // 25_000, minlength=world)
+    assert contiguous[0] > 3 * contiguous[1:].max()
+
+
+def test_exchange_choice_is_static_and_by_bound():
+    # no device data: the choice follows P, the arrays and the bound
+    assert distributed.choose_exchange(1_000_000, 3, 8, 1_000_000) == "reduce_scatter"
+    # fixed blocks: every destination may receive all of a rank's occupied
+    # partitions, so sparse pays off when the bound is well under P / R
+    assert distributed.choose_exchange(100_000_000, 4, 8, 10_000_000) == "reduce_scatter"
+    assert distributed.choose_exchange(100_000_000, 4, 8, 1_000_000) == "all_to_all"
+    assert distributed.choose_exchange(100_000_000, 4, 8, 1_000_000, "reduce_scatter") == \
+        "reduce_scatter"
+    with pytest.raises(ValueError):
+        distributed.choose_exchange(10, 1, 2, 10, "ring")
+    b = distributed.exchange_bytes(100_000_000, 1_000_000, 5, 8)
+    assert b["all_to_all"] * 2 < b["reduce_scatter"]
+    # the bound: records, privacy ids x l0, P
+    assert distributed.occupancy_bound(10**6, 10**9, 10**7, 8) == 10**6
+    assert distributed.occupancy_bound(10**8, 10**9, 10**6, 8) == 8 * 10**6
+    assert distributed.occupancy_bound(10**8, 5000, 0, 8) == 5000
 
 
 def test_shard_is_deterministic_and_balanced():

@@ -57,7 +57,7 @@ def test_rccl_reduce_scatter_partials_one_rank(built):
     stream = torch.cuda.current_stream(dev)
     lo, n = ctx.reduce_scatter_partials(full, sl, stream.cuda_stream)
     torch.cuda.synchronize()
-    assert (lo, n) == (0, P)
+    assert (lo, n) == (0, P)   # one rank owns every partition
     for k, v in out.items():
         assert torch.equal(v, parts[k]), k
     assert int(out["rows"].sum()) > 0
@@ -75,15 +75,17 @@ def test_reduce_scatter_without_communicator_fails(built):
 
 @pytest.mark.parametrize("R", [2, 3])
 def test_pack_unpack_layout_for_several_ranks(built, R):
-    """the [rank][array][S] layout, the zero padding past P and
-    the rank * S slice offsets of the C-ABI pack equal the torch path's
-    (distributed.reduce_scatter_partials); R emulated ranks' packs summed on
-    the host and unpacked per rank give every rank its slice of the sum."""
+    """The C-ABI pack layout equals the torch path's
+    (distributed.reduce_scatter_partials): rank r's block is [array][S] with
+    element i = partition i * R + r (interleaved ownership), zero padded past
+    P, then the sender's error flag; R emulated ranks' packs summed on the
+    host and unpacked per rank give every rank its partitions of the sum."""
     from pipelinedp_amd import _native
     backend, parts, P = _aggregate()
     ctx = backend.ctx
     dev = parts["rows"].device
     names = [k for k in ("rows", "count", "sum", "nsum", "nsq") if parts.get(k) is not None]
+    A = len(names)
     S = (P + R - 1) // R
     stream = torch.cuda.current_stream(dev).cuda_stream
     ptr = lambda d, k: d[k].data_ptr() if d.get(k) is not None else None  # noqa: E731
@@ -93,14 +95,15 @@ def test_pack_unpack_layout_for_several_ranks(built, R):
     for r in range(R):
         full = _native.Partials(P, *(ptr(ranks[r], k) for k in ("rows", "count", "sum", "nsum",
                                                                   "nsq")))
-        pack = torch.full((R, len(names), S), -5.0, dtype=torch.float64, device=dev)
+        pack = torch.full((R, A * S + 1), -5.0, dtype=torch.float64, device=dev)
         ctx.pack_partials(full, R, pack.data_ptr(), stream)
         torch.cuda.synchronize()
-        expect = torch.zeros((len(names), R * S), dtype=torch.float64, device=dev)
+        expect = torch.zeros((R, A * S + 1), dtype=torch.float64, device=dev)
         for j, k in enumerate(names):
-            expect[j, :P] = ranks[r][k].to(torch.float64)
-        expect = expect.view(len(names), R, S).transpose(0, 1)
-        assert torch.equal(pack, expect), r
+            x = torch.zeros(R * S, dtype=torch.float64, device=dev)
+            x[:P] = ranks[r][k].to(torch.float64)
+            expect[:, j * S:(j + 1) * S] = x.view(S, R).t()
+        assert torch.equal(pack, expect), r      # error slot 0.0: no bounding error
         packs.append(pack)
     total = sum(packs)
     scale = R * (R + 1) // 2
@@ -110,10 +113,42 @@ def test_pack_unpack_layout_for_several_ranks(built, R):
         sl = _native.Partials(S, *(ptr(out, k) for k in ("rows", "count", "sum", "nsum", "nsq")))
         lo, n = ctx.unpack_partials(part.data_ptr(), P, R, r, sl, stream)
         torch.cuda.synchronize()
-        assert lo == r * S and n == min(P, lo + S) - lo
+        own = torch.arange(r, P, R, device=dev)
+        assert lo == r and n == own.numel()
         for k in names:
-            want = parts[k][lo:lo + n] * scale
+            want = parts[k][own] * scale
             if parts[k].dtype == torch.int64:
                 assert torch.equal(out[k][:n], want), (r, k)
             else:
                 assert torch.allclose(out[k][:n], want, rtol=1e-12, atol=1e-9), (r, k)
+
+
+def test_error_flag_travels_and_fails_compaction(built):
+    """a rank whose bounding latched an internal error must fail
+    every rank's release.  The flag of a sender travels in the exchange
+    (dpg_unpack_partials / dpg_import_error latch it) and the receiver's
+    dpg_compact_kept then fails; a clean block leaves it unharmed."""
+    from pipelinedp_amd import _native
+    backend, parts, P = _aggregate()
+    ctx = backend.ctx
+    dev = parts["rows"].device
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    flag = torch.full((1,), -1.0, dtype=torch.float64, device=dev)
+    ctx.export_error(flag.data_ptr(), stream)
+    torch.cuda.synchronize()
+    assert float(flag) == 0.0                     # the aggregate above was clean
+    keep = torch.ones(8, dtype=torch.uint8, device=dev)
+    ids = torch.empty(8, dtype=torch.int64, device=dev)
+    zero = torch.zeros(2, dtype=torch.float64, device=dev)
+    ctx.import_error(zero.data_ptr(), 2, stream)
+    assert ctx.compact(keep.data_ptr(), None, 8, 0, ids.data_ptr(), None, stream) == 8
+    # an unpacked block whose error slot is set (another rank's flag)
+    names = [k for k in ("rows", "count", "sum") if parts.get(k) is not None]
+    part = torch.zeros(len(names) * P + 1, dtype=torch.float64, device=dev)
+    part[-1] = 1.0
+    out = {k: torch.empty(P, dtype=parts[k].dtype, device=dev) for k in names}
+    sl = _native.Partials(P, *(out[k].data_ptr() if k in out else None
+                               for k in ("rows", "count", "sum", "nsum", "nsq")))
+    ctx.unpack_partials(part.data_ptr(), P, 1, 0, sl, stream)
+    with pytest.raises(_native.NativeError, match="internal"):
+        ctx.compact(keep.data_ptr(), None, 8, 0, ids.data_ptr(), None, stream)

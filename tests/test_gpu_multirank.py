@@ -53,8 +53,8 @@ def _release(pid, pk, val, offset, group):
     acc.compute_budgets()
     res.nonce = NONCE
     out = res.materialize()
-    part, lo, n = res.last_slice
-    return (lo, n, {k: v.cpu().numpy() for k, v in part.items() if v is not None},
+    part, lo, stride, n = res.last_slice
+    return (lo, stride, n, {k: v.cpu().numpy() for k, v in part.items() if v is not None},
             out.partition_ids.cpu().numpy(), out.values.cpu().numpy(), res.nonce)
 
 
@@ -94,14 +94,16 @@ def test_two_ranks_equal_one_rank(built):
                 p.kill()
     assert all(p.exitcode == 0 for p in procs)
     pid, pk, val, _ = _dataset()
-    lo1, n1, full, ids1, vals1, nonce1 = _release(pid, pk, val, 0, None)
-    assert (lo1, n1) == (0, P)
-    for rank, lo, n, part, ids, vals, nonce in res:
+    lo1, s1, n1, full, ids1, vals1, nonce1 = _release(pid, pk, val, 0, None)
+    assert (lo1, s1, n1) == (0, 1, P)
+    for rank, lo, stride, n, part, ids, vals, nonce in res:
         assert nonce == NONCE
-        assert lo == rank * (P // WORLD) and n == P // WORLD
-        assert np.array_equal(part["rows"], full["rows"][lo:lo + n])
-        assert np.array_equal(part["count"], full["count"][lo:lo + n])
-        assert np.allclose(part["sum"], full["sum"][lo:lo + n], rtol=1e-12, atol=1e-9)
+        # interleaved ownership: rank r owns r, r + WORLD, ...
+        assert lo == rank and stride == WORLD and n == P // WORLD
+        own = np.arange(rank, P, WORLD)
+        assert np.array_equal(part["rows"], full["rows"][own])
+        assert np.array_equal(part["count"], full["count"][own])
+        assert np.allclose(part["sum"], full["sum"][own], rtol=1e-12, atol=1e-9)
         # every rank holds the gathered release: same set, same values
         assert np.array_equal(np.sort(ids), np.sort(ids1))
         o, o1 = np.argsort(ids), np.argsort(ids1)
