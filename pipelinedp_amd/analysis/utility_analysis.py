@@ -105,9 +105,10 @@ def _sample_bound(prob: float) -> int:
 
 
 def _keep_by_hash(key, bound: int) -> bool:
-    """sampling_utils.ValueSampler.keep (sampling_utils.py:32-51)."""
-    if isinstance(key, np.generic):  # hash what the reference's row key would print
-        key = key.item()
+    """sampling_utils.ValueSampler.keep (sampling_utils.py:32-51): the
+    repr of the key exactly as the user's rows hold it (columnar.decode_keys
+    returns Python scalars for integer columns and the row objects for row
+    input)."""
     h = int(hashlib.sha1(repr(key).encode()).hexdigest()[:16], 16)
     return h < bound
 

@@ -209,7 +209,11 @@ def encode(col, extractors, device: torch.device, need_values: bool,
     key_table = None
     pk_ids = None
     public_ids = None
-    if _integer_like(pk):
+    # rows whose partition keys are numpy scalars keep those objects as the
+    # key table: results and the utility analysis' partition sampler then see
+    # the user's own keys (repr np.int64(5), as the reference's rows print)
+    np_row_keys = isinstance(pk, list) and any(isinstance(k, np.generic) for k in pk)
+    if _integer_like(pk) and not np_row_keys:
         pk_t = _to_tensor(pk, device).to(torch.int64)
         if hint is not None:
             P = int(hint)

@@ -54,6 +54,10 @@ constexpr uint32_t kSkPkBits = 24;  // partition-key bits of the sort key
 #define DPG_SORT_PACKED 1  // narrow kernel: keys with the position packed in, no payload
 #endif
 constexpr uint64_t kSkPad = ~0ull;  // padding elements (real keys have bit 63 clear)
+#ifndef DPG_SORT_LATE
+#define DPG_SORT_LATE 1  // value gathers of over-full pairs after their mcpp sample
+#endif
+constexpr bool kSortLate = DPG_SORT_LATE != 0;
 
 // The wave's LDS working set is kept under 10 KB (COUNT / SUM items) so that
 // 16 waves share a CU: the kernel is latency-bound per wave (same-box A/B,
@@ -475,7 +479,10 @@ __device__ __forceinline__ int sort_chunk(uint32_t nc, char *smem, const BoundPa
         const bool ov = sample && kp && len[j] > bp.mcpp;
         overm |= ov ? 1u << j : 0u;
         maxlen = max(maxlen, ov ? len[j] : 0u);
-        v[j] = (need_v && kp) ? bp.value[idx[j]] : 0.0;
+        // records of kept pairs within mcpp gather now; those of over-full
+        // pairs only once the sample below has kept them (DPG_SORT_LATE 0:
+        // every record of a kept pair gathers here)
+        v[j] = (need_v && kp && (!kSortLate || !ov)) ? bp.value[idx[j]] : 0.0;
     }
     uint32_t keepm = kpm;
     maxlen = __builtin_amdgcn_readfirstlane(wave_max_u32(maxlen));
@@ -503,6 +510,13 @@ __device__ __forceinline__ int sort_chunk(uint32_t nc, char *smem, const BoundPa
                 below += (t + 1 < len[j] && y1 < mine) ? 1u : 0u;
             }
             if (ov && below >= bp.mcpp) keepm &= ~(1u << j);
+        }
+        if constexpr (kSortLate) {
+            if (need_v) {
+#pragma unroll
+                for (int j = 0; j < E; ++j)
+                    if ((overm & keepm) >> j & 1u) v[j] = bp.value[idx[j]];
+            }
         }
     }
     mark(bp, 3, clk);

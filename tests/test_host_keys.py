@@ -2,6 +2,8 @@
 treat tensor / numpy keys by value, as the reference's hashable row keys
 are (private_contribution_bounds.py:93 len(set(partitions));
 sampling_utils.py:32-51 ValueSampler hashes repr(key))."""
+import hashlib
+
 import numpy as np
 import torch
 
@@ -28,13 +30,37 @@ def test_distinct_partitions_by_value_for_every_container():
     assert _calc(iter(keys))._number_of_partitions() == want
 
 
+def _ref_keep(v, rate):
+    """The reference ValueSampler (sampling_utils.py:30-51), restated."""
+    return int(hashlib.sha1(repr(v).encode()).hexdigest()[:16], 16) < int(round(2**64 * rate))
+
+
 def test_decoded_keys_are_python_scalars_and_sample_like_row_keys():
     table = np.array([5, 9, 11], dtype=np.int64)
     keys = columnar.decode_keys(np.array([2, 0]), table)
     assert keys == [11, 5] and all(type(k) is int for k in keys)
     assert repr(keys[1]) == "5"
-    for bound in (ua._sample_bound(0.3), ua._sample_bound(0.7)):
-        for k in (0, 5, 123456789):
-            assert ua._keep_by_hash(np.int64(k), bound) == ua._keep_by_hash(k, bound)
+    for rate in (0.3, 0.7):
+        bound = ua._sample_bound(rate)
+        for k in (0, 5, 123456789, "pk7", np.int64(5), np.int32(123456789)):
+            # keys are hashed exactly as given, like the reference's row keys
+            assert ua._keep_by_hash(k, bound) == _ref_keep(k, rate)
     # object key tables (strings) pass through unchanged
     assert columnar.decode_keys(np.array([1]), ["a", "b"]) == ["b"]
+
+
+def test_numpy_scalar_row_keys_come_back_as_given():
+    """rows whose partition keys are numpy scalars keep those
+    objects, so the partition sampler hashes repr(np.int64(5)) as the
+    reference does and the results carry the user's key objects."""
+    rows = [(1, np.int64(5), 1.0), (2, np.int64(9), 2.0), (3, np.int64(5), 3.0)]
+    ex = type("Ex", (), dict(privacy_id_extractor=staticmethod(lambda r: r[0]),
+                             partition_extractor=staticmethod(lambda r: r[1]),
+                             value_extractor=staticmethod(lambda r: r[2])))
+    enc = columnar.encode(rows, ex, torch.device("cpu"), True)
+    keys = columnar.decode_keys(np.arange(enc.n_partitions), enc.key_table)
+    assert keys == [np.int64(5), np.int64(9)] and all(type(k) is np.int64 for k in keys)
+    assert [repr(k) for k in keys] == [repr(np.int64(5)), repr(np.int64(9))]
+    # plain Python integer rows stay dense ids decoded as Python ints
+    enc2 = columnar.encode([(1, 5, 1.0), (2, 9, 2.0)], ex, torch.device("cpu"), True)
+    assert enc2.key_table is None

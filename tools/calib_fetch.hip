@@ -55,14 +55,27 @@ int main() {
     (void)hipMemset(a, 1, bytes);
     const size_t n8 = bytes / 8;
     const size_t n_reads = (size_t)1 << 26;  // 64 Mi gathers
+    // the second repetition is timed: a gather's true HBM cost shows in its
+    // rate against the streaming read's (both far beyond the caches)
+    hipEvent_t ev[5];
+    for (auto &e : ev) (void)hipEventCreate(&e);
     for (int rep = 0; rep < 2; ++rep) {
+        (void)hipEventRecord(ev[0]);
         k_read8<<<4096, 256>>>(a, n8, out);
+        (void)hipEventRecord(ev[1]);
         k_read16<<<4096, 256>>>(reinterpret_cast<const uint4 *>(a), bytes / 16, out);
+        (void)hipEventRecord(ev[2]);
         k_gather8<<<4096, 256>>>(a, bytes / 64, n_reads, out);
+        (void)hipEventRecord(ev[3]);
         k_write8<<<4096, 256>>>(a, n8);
+        (void)hipEventRecord(ev[4]);
     }
     (void)hipDeviceSynchronize();
-    std::printf("{\"read_bytes\": %zu, \"gather_reads\": %zu, \"write_bytes\": %zu}\n", bytes,
-                n_reads, bytes);
+    float ms[4];
+    for (int i = 0; i < 4; ++i) (void)hipEventElapsedTime(&ms[i], ev[i], ev[i + 1]);
+    std::printf("{\"read_bytes\": %zu, \"gather_reads\": %zu, \"write_bytes\": %zu, "
+                "\"ms\": {\"k_read8\": %.4f, \"k_read16\": %.4f, \"k_gather8\": %.4f, "
+                "\"k_write8\": %.4f}}\n",
+                bytes, n_reads, bytes, ms[0], ms[1], ms[2], ms[3]);
     return 0;
 }
