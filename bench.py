@@ -246,8 +246,8 @@ def stage_design_bytes(stage: str, n: int, rec: int, item: int, kept_recs: int,
         return (16 + rec) * n             # pid + pk in, packed record out
     if stage in ("partition2:hist", "refine:hist"):
         return rec * n
-    if stage in ("partition2:scatter", "refine:scatter"):
-        return 2 * rec * n
+    if stage in ("partition2:scatter", "refine:scatter", "partition2:team"):
+        return 2 * rec * n                # records in and out (team level 2: no hist pass)
     if stage == "bounding":               # all bounding kernels: records in, kept
         return rec * n + 8 * kept_recs + item * kept_pairs  # values gathered, items out
     if stage in ("items:hist", "items2:hist"):

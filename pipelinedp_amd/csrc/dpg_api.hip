@@ -15,6 +15,7 @@
 #include <rccl/rccl.h>  // types and enums only: the functions are resolved by dlsym
 
 #include <algorithm>
+#include <cstddef>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -33,6 +34,7 @@
 #include "dpg_select.h"
 #include "dpg_sortb.h"
 #include "dpg_sortmw.h"
+#include "dpg_team.h"
 #include "dpg_utility.h"
 #include "dpg_wave.h"
 
@@ -45,6 +47,9 @@ constexpr uint32_t kBucketTarget = 256;  // average records per fine bucket
 // records per sub-tile); refine and item levels keep <= 11
 constexpr uint32_t kMaxB1 = 11, kMaxB2 = 12, kMaxBR = 11;
 constexpr uint32_t kChunkGroup = 32;     // fine buckets per packing thread
+// Status of bound_and_reduce when a team level-2 barrier timed out (err bit
+// 8): the caller redoes level 2 with the histogram path.
+constexpr int kRedoLevel2 = -100;
 
 struct Buf {
     void *p = nullptr;
@@ -91,6 +96,10 @@ struct dpg_ctx {
     char *stage_buf = nullptr;
     size_t stage_cap = 0, stage_head = 0;
     std::map<hipStream_t, hipEvent_t> stage_done;
+    // level-1 bucket counts copied to the host while the level-1 scatter
+    // runs (the team level-2 decision, see pipeline())
+    uint32_t *pin_tot = nullptr;
+    hipEvent_t tot_ev = nullptr;
 };
 
 namespace {
@@ -287,7 +296,7 @@ int run_level_grouped(dpg_ctx *ctx, hipStream_t s, const Src &src, uint32_t S,
                       const int64_t *seg_start, const uint32_t *seg_cnt, const int64_t *seg_cnt64,
                       int64_t n_upper, uint32_t F, uint32_t bits, Rec *out, const char *tag,
                       int64_t **base_out, uint32_t **tot_out, uint32_t *ntiles_dev,
-                      const int64_t *out_start) {
+                      const int64_t *out_start, uint32_t *host_tot = nullptr) {
     int st = DPG_OK;
     const int64_t sub = (int64_t)kScatThreads * IPT;
     const bool single = S == 1 && !seg_start && !seg_cnt;  // level 1: all n records
@@ -343,6 +352,13 @@ int run_level_grouped(dpg_ctx *ctx, hipStream_t s, const Src &src, uint32_t S,
     LAUNCH_CHECK();
     k_digit_base<<<S, 1024, 0, s>>>(out_start ? out_start : seg_start, F, tot, base);
     LAUNCH_CHECK();
+    if (host_tot) {
+        // the segment totals reach the host while the scatter runs
+        if (!ctx->tot_ev && hipEventCreateWithFlags(&ctx->tot_ev, hipEventDisableTiming) != hipSuccess)
+            return fail(ctx, DPG_ERR_HIP, "hipEventCreate (totals)");
+        HIP_TRY(hipMemcpyAsync(host_tot, tot, (size_t)S * F * 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipEventRecord(ctx->tot_ev, s));
+    }
     constexpr size_t lds = scatter_lds<Src, Rec, IPT, FMAX>();
     static_assert(lds <= 160 * 1024, "scatter LDS");
     auto kern = bits > agg_bits() ? k_scatter<Src, Rec, IPT, FMAX, false> : k_scatter<Src, Rec, IPT, FMAX, true>;
@@ -364,13 +380,14 @@ int run_level(dpg_ctx *ctx, hipStream_t s, const Src &src, uint32_t S, const int
               const uint32_t *seg_cnt, const int64_t *seg_cnt64, int64_t n_upper, uint32_t F,
               uint32_t bits, Rec *out, const char *tag, int64_t **base_out, uint32_t **tot_out,
               uint32_t *ntiles_dev, const int64_t *out_start = nullptr, bool xcd_local = false,
-              int subs = 1, bool grouped = false) {
+              int subs = 1, bool grouped = false, uint32_t *host_tot = nullptr) {
     int st = DPG_OK;
     if (F > (uint32_t)FMAX) return fail(ctx, DPG_ERR_HIP, "internal: digit fan-out too large");
     const int64_t sub = (int64_t)kScatThreads * IPT;
     if (grouped) return run_level_grouped<Src, Rec, IPT, FMAX>(ctx, s, src, S, seg_start, seg_cnt,
                                                                seg_cnt64, n_upper, F, bits, out, tag,
-                                                               base_out, tot_out, ntiles_dev, out_start);
+                                                               base_out, tot_out, ntiles_dev, out_start,
+                                                               host_tot);
     // XCD-local mode: `subs` sub-tiles per tile, tiles of a segment on one
     // XCD (every tile carries a digit histogram: tiny tiles cost histogram
     // traffic and scan time)
@@ -506,6 +523,7 @@ struct PaOut {
 };
 
 __global__ void k_set_i64(int64_t *p, int64_t v) { *p = v; }
+__global__ void k_set_bits(uint32_t *p, uint32_t bits) { atomicOr(p, bits); }
 
 // Bounding of the fine buckets + merge of the kept pairs per partition (or,
 // for the pre-aggregate, the pairs sorted by partition key).
@@ -546,6 +564,7 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     if (hctl.err & 1u)
         return fail(ctx, DPG_ERR_KEY_RANGE,
                     "privacy id outside its declared range or partition key outside [0, P)");
+    if (hctl.err & 8u) return kRedoLevel2;
     uint4 *chunk_list = chunks;
     size_t chunk_cap = B;  // entries of chunk_list
     const uint4 *mchunk_list = mchunks;
@@ -1018,6 +1037,40 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     return DPG_OK;
 }
 
+// Level 2 by teams of workgroups (dpg_team.h): S level-1 buckets, each
+// <= (n_cu / 8) * kTeamSub records (the caller checked the level-1 totals).
+template <class R>
+int run_team_level2(dpg_ctx *ctx, hipStream_t s, const SrcAoS<R> &src, uint32_t S, uint32_t F2,
+                    const int64_t *seg_start, const uint32_t *seg_cnt, R *out, Control *ctl,
+                    int64_t **base_out, uint32_t **tot_out) {
+    int st = DPG_OK;
+    const uint32_t F = kTeamF;
+    const size_t words = (size_t)8 * 3 * F + 8 * kTeamArriveStride + 32;
+    WS(tw, uint32_t, "team.sync", words);
+    WS(base, int64_t, "partition2.base", (size_t)S * F2);
+    WS(tot, uint32_t, "partition2.tot", (size_t)S * F2);
+    HIP_TRY(hipMemsetAsync(tw, 0, words * 4, s));
+    uint32_t *abort_flag = tw + (size_t)8 * 3 * F + 8 * kTeamArriveStride;
+    const TeamSync ts{tw, tw + (size_t)8 * 3 * F, abort_flag, &ctl->err};
+    if (std::getenv("DPG_DEBUG_TEAM_ABORT")) {
+        // test hook: the team gives up at its first barrier, as after a
+        // timeout (abort flag and err bit 8), so the host redoes level 2
+        const uint32_t one = 1;
+        UPLOAD(abort_flag, &one, 4);
+        k_set_bits<<<1, 1, 0, s>>>(&ctl->err, 8u);
+        LAUNCH_CHECK();
+    }
+    const void *k = (const void *)k_part2_team<R>;
+    (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)team_lds<R>());
+    stage(ctx, s, "partition2:team");
+    k_part2_team<R><<<(unsigned)ctx->n_cu, kScatThreads, team_lds<R>(), s>>>(
+        src, seg_start, seg_cnt, S, F2, out, base, tot, ts);
+    LAUNCH_CHECK();
+    *base_out = base;
+    *tot_out = tot;
+    return DPG_OK;
+}
+
 template <class R>
 int pipeline(dpg_ctx *ctx, hipStream_t s, const int64_t *pid, const int64_t *pk,
              const double *value, int64_t n, const dpg_bound_params *p, const dpg_partials *out,
@@ -1064,14 +1117,45 @@ int pipeline(dpg_ctx *ctx, hipStream_t s, const int64_t *pid, const int64_t *pk,
     const bool l1_grp = env_int("DPG_L1_GRP", DPG_L1_GRP) != 0;
     const bool l2_grp = env_int("DPG_L2_GRP", DPG_L2_GRP) != 0;
     const uint32_t shift2 = pl.pkbits + (pl.kbits - pl.b1) - pl.b2;
+    // level 2 by teams of workgroups (dpg_team.h, no histogram pass): 8-byte
+    // records, an 11-bit level 2, every workgroup of a one-per-CU launch
+    // resident, and -- checked on the level-1 totals, which reach the host
+    // while the level-1 scatter runs -- every level-1 bucket within a team's
+    // registers.  DPG_TEAM_L2=0: the grouped histogram path.
+    const uint32_t team_T = (uint32_t)ctx->n_cu / 8;
+    bool team = sizeof(R) == 8 && pl.b2 >= 6 && pl.b2 <= kMaxB1 && ctx->n_cu % 8 == 0 && team_T > 0 && l1_grp &&
+                env_int("DPG_TEAM_L2", 1) != 0;
+    if (team) {
+        int occ = 0;
+        const void *tk = (const void *)k_part2_team<R>;
+        (void)hipFuncSetAttribute(tk, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)team_lds<R>());
+        team = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, tk, kScatThreads,
+                                                            team_lds<R>()) == hipSuccess &&
+               occ >= 1;
+    }
+    if (team && !ctx->pin_tot &&
+        hipHostMalloc((void **)&ctx->pin_tot, (size_t)4 * 4096, hipHostMallocDefault) != hipSuccess) {
+        ctx->pin_tot = nullptr;
+        team = false;
+    }
     int r = run_level<SrcSoAKey<R>, R, Ipt<R>::L1, 2048>(ctx, s, s1, 1u, nullptr, nullptr,
                                                          &ctl->n_scalar, n, F1, pl.b1, recA,
                                                          "partition1", &bstart, &bcnt, &ctl->ntiles[0],
-                                                         nullptr, l1_xcd, l1_subs, l1_grp);
+                                                         nullptr, l1_xcd, l1_subs, l1_grp,
+                                                         team ? ctx->pin_tot : nullptr);
     if (r) return r;
+    if (team) {
+        HIP_TRY(hipEventSynchronize(ctx->tot_ev));
+        uint32_t mx = 0;
+        for (uint32_t d = 0; d < F1; ++d) mx = std::max(mx, ctx->pin_tot[d]);
+        team = (uint64_t)mx <= (uint64_t)team_T * kTeamSub;
+    }
+    const int64_t *bstart1 = bstart;
+    const uint32_t *bcnt1 = bcnt;
     const R *cur = recA;
     uint32_t B = F1;
-    if (pl.b2 > 0) {
+    auto level2_grouped = [&]() -> int {
         // ---- level 2: next b2 hash bits inside every level-1 bucket
         const uint32_t F2 = 1u << pl.b2;
         SrcAoS<R> s2{recA, f, shift2, F2 - 1};
@@ -1084,15 +1168,25 @@ int pipeline(dpg_ctx *ctx, hipStream_t s, const int64_t *pid, const int64_t *pk,
 #ifndef DPG_L2_XCD
 #define DPG_L2_XCD 1
 #endif
-        r = pl.b2 > 11
-                ? run_level<SrcAoS<R>, R, Ipt<R>::LW, 4096>(ctx, s, s2, F1, bstart, bcnt, nullptr, n,
+        int r = pl.b2 > 11
+                ? run_level<SrcAoS<R>, R, Ipt<R>::LW, 4096>(ctx, s, s2, F1, bstart1, bcnt1, nullptr, n,
                                                              F2, pl.b2, recB, "partition2", &bstart,
                                                              &bcnt, &ctl->ntiles[1], nullptr,
                                                              DPG_L2_XCD != 0, l2_subs, l2_grp)
-                : run_level<SrcAoS<R>, R, Ipt<R>::LN, 2048>(ctx, s, s2, F1, bstart, bcnt, nullptr, n,
+                : run_level<SrcAoS<R>, R, Ipt<R>::LN, 2048>(ctx, s, s2, F1, bstart1, bcnt1, nullptr, n,
                                                              F2, pl.b2, recB, "partition2", &bstart,
                                                              &bcnt, &ctl->ntiles[1], nullptr,
                                                              DPG_L2_XCD != 0, l2_subs, l2_grp);
+        return r;
+    };
+    if (pl.b2 > 0) {
+        const uint32_t F2 = 1u << pl.b2;
+        if (team) {
+            SrcAoS<R> s2{recA, f, shift2, F2 - 1};
+            r = run_team_level2<R>(ctx, s, s2, F1, F2, bstart1, bcnt1, recB, ctl, &bstart, &bcnt);
+        } else {
+            r = level2_grouped();
+        }
         if (r) return r;
         cur = recB;
         B = F1 * F2;
@@ -1104,27 +1198,43 @@ int pipeline(dpg_ctx *ctx, hipStream_t s, const int64_t *pid, const int64_t *pk,
     bp.value = value;
     bp.err = &ctl->err;
     const bool key32 = pl.pkbits <= 21;  // (pid slot < 2^10) << pkbits | pk < 2^31
-    if (pa)
-        return key32 ? bound_and_reduce<R, uint32_t, ItemPA>(ctx, s, pl, cur, bstart, bcnt, B, bp,
-                                                             n, out, ctl, pa)
-                     : bound_and_reduce<R, uint64_t, ItemPA>(ctx, s, pl, cur, bstart, bcnt, B, bp,
-                                                             n, out, ctl, pa);
-    // MEAN / VARIANCE without SUM (and without per-partition sum clipping):
-    // 24-byte items with the normalised moments only
-    if (var && !(p->metric_mask & DPG_M_SUM) && p->sum_mode != DPG_SUM_CLIP_PARTITION)
-        return key32 ? bound_and_reduce<R, uint32_t, ItemV>(ctx, s, pl, cur, bstart, bcnt, B, bp,
-                                                            n, out, ctl, nullptr)
-                     : bound_and_reduce<R, uint64_t, ItemV>(ctx, s, pl, cur, bstart, bcnt, B, bp,
-                                                            n, out, ctl, nullptr);
-    if (var)
-        return key32 ? bound_and_reduce<R, uint32_t, Item32>(ctx, s, pl, cur, bstart, bcnt, B, bp,
-                                                             n, out, ctl, nullptr)
-                     : bound_and_reduce<R, uint64_t, Item32>(ctx, s, pl, cur, bstart, bcnt, B, bp,
-                                                             n, out, ctl, nullptr);
-    return key32 ? bound_and_reduce<R, uint32_t, Item16>(ctx, s, pl, cur, bstart, bcnt, B, bp, n,
-                                                         out, ctl, nullptr)
-                 : bound_and_reduce<R, uint64_t, Item16>(ctx, s, pl, cur, bstart, bcnt, B, bp, n,
-                                                         out, ctl, nullptr);
+    auto bound = [&]() -> int {
+        if (pa)
+            return key32 ? bound_and_reduce<R, uint32_t, ItemPA>(ctx, s, pl, cur, bstart, bcnt, B, bp,
+                                                                 n, out, ctl, pa)
+                         : bound_and_reduce<R, uint64_t, ItemPA>(ctx, s, pl, cur, bstart, bcnt, B, bp,
+                                                                 n, out, ctl, pa);
+        // MEAN / VARIANCE without SUM (and without per-partition sum clipping):
+        // 24-byte items with the normalised moments only
+        if (var && !(p->metric_mask & DPG_M_SUM) && p->sum_mode != DPG_SUM_CLIP_PARTITION)
+            return key32 ? bound_and_reduce<R, uint32_t, ItemV>(ctx, s, pl, cur, bstart, bcnt, B, bp,
+                                                                n, out, ctl, nullptr)
+                         : bound_and_reduce<R, uint64_t, ItemV>(ctx, s, pl, cur, bstart, bcnt, B, bp,
+                                                                n, out, ctl, nullptr);
+        if (var)
+            return key32 ? bound_and_reduce<R, uint32_t, Item32>(ctx, s, pl, cur, bstart, bcnt, B, bp,
+                                                                 n, out, ctl, nullptr)
+                         : bound_and_reduce<R, uint64_t, Item32>(ctx, s, pl, cur, bstart, bcnt, B, bp,
+                                                                 n, out, ctl, nullptr);
+        return key32 ? bound_and_reduce<R, uint32_t, Item16>(ctx, s, pl, cur, bstart, bcnt, B, bp, n,
+                                                             out, ctl, nullptr)
+                     : bound_and_reduce<R, uint64_t, Item16>(ctx, s, pl, cur, bstart, bcnt, B, bp, n,
+                                                             out, ctl, nullptr);
+    };
+    r = bound();
+    if (r == kRedoLevel2) {
+        // a team barrier timed out (workgroups not co-resident): level 2 again
+        // with the histogram path, the chunk counters reset
+        std::fprintf(stderr, "[dpg] team level 2 timed out; redone with the histogram path\n");
+        HIP_TRY(hipMemsetAsync(&ctl->err, 0, 4, s));
+        HIP_TRY(hipMemsetAsync(&ctl->n_chunks, 0,
+                               offsetof(Control, pid_lo) - offsetof(Control, n_chunks), s));
+        r = level2_grouped();
+        if (r) return r;
+        r = bound();
+        if (r == kRedoLevel2) return fail(ctx, DPG_ERR_HIP, "internal: level-2 redo flagged again");
+    }
+    return r;
 }
 
 // dpg_bound_aggregate / dpg_preaggregate after argument checks: pid range,
@@ -1340,6 +1450,8 @@ void dpg_ctx_destroy(dpg_ctx *c) {
         (void)hipEventDestroy(kv.second);
     }
     if (c->stage_buf) (void)hipHostFree(c->stage_buf);
+    if (c->tot_ev) (void)hipEventDestroy(c->tot_ev);
+    if (c->pin_tot) (void)hipHostFree(c->pin_tot);
     delete c;
 }
 

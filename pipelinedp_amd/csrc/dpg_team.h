@@ -1,0 +1,269 @@
+// dpg_team.h -- level-2 partitioning without a histogram pass (gfx950).
+//
+// The grouped level 2 of dpg_partition.h reads every record twice: once in
+// k_hist (the digit counts of its level-1 bucket) and once in k_scatter.
+// Here the digit counts come from the records the scatter holds anyway:
+//
+// * a TEAM is the workgroups w = x, x + 8, x + 16, ... of one persistent
+//   launch of one workgroup per CU (round-robin dispatch puts them on XCD x,
+//   so the team shares one L2); team x takes the level-1 buckets x, x + 8,
+//   ... in order;
+// * each member loads its 1/T share of the bucket (<= kTeamSub records)
+//   into registers, ranks it by digit in LDS and adds its digit counts to
+//   the team's totals with one atomic per digit -- the returned old value is
+//   the member's run offset inside the digit (arrival order, as the grouped
+//   scatter's reservations);
+// * after a team barrier every member reads the totals, scans them into the
+//   bucket's digit starts and writes its runs, staged through LDS as in
+//   k_scatter (member 0 also writes the fine buckets' starts and counts).
+//
+// The records therefore cross HBM once in and once out; the barrier replaces
+// the histogram pass.  Totals are triple-buffered per team (a member zeroes
+// the buffer of the bucket after next once every member has read the one
+// before), so one barrier per bucket suffices.  The barrier is bounded: a
+// member that waits longer than kTeamTimeout (co-residency lost) raises
+// err bit 8 and the abort flag, every member leaves, and the host redoes
+// the level with the histogram path.
+#pragma once
+
+#include "dpg_partition.h"
+
+namespace dpg {
+
+constexpr int kTeamIPT = 16;                       // records per thread
+constexpr uint32_t kTeamF = 2048;                  // digits (11 bits)
+constexpr int kTeamSub = kScatThreads * kTeamIPT;  // records per member per bucket
+constexpr uint64_t kTeamTimeout = 50000000ull;     // wall_clock64 ticks (100 MHz): 0.5 s
+constexpr uint32_t kTeamArriveStride = 32;         // counters on separate 128-B lines
+
+struct TeamSync {
+    uint32_t *tot;     // [8][3][kTeamF] digit totals per team, triple-buffered (zeroed)
+    uint32_t *arrive;  // [8 * kTeamArriveStride] arrivals per team (zeroed)
+    uint32_t *abort;   // nonzero: a barrier timed out, every member leaves
+    uint32_t *err;     // Control::err; bit 8 = team barrier timeout
+};
+
+template <class R>
+constexpr size_t team_lds() {
+    return sizeof(R) * (kTeamSub + 1) + (size_t)kTeamF * 12 + 4 * 4 + 64;
+}
+
+__device__ __forceinline__ uint32_t ld_agent(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// All members of `team` have arrived `target` times in total.  Returns false
+// when the team gave up (timeout or another member's abort).
+//
+// Hand-off form (MI355X_MICROARCH.md, inter-workgroup visibility, first row
+// of the sc1 table): the only data the members exchange are the digit totals,
+// written by agent-scope atomics (adds; the zeroing by atomic stores) and
+// read by sc1 loads (ld_agent), so no L2 write-back or L1 invalidate is
+// needed -- only that every wave's atomics have completed before one lane
+// adds to the arrival counter behind a workgroup barrier, and that the
+// poll is an sc1 load.  (Agent-scope fences here -- __threadfence in every
+// thread, a release add, an acquire per poll -- wrote back and invalidated
+// the XCD L2 that holds the scattered runs: 20.5 ms instead of ~4 ms.)
+__device__ __forceinline__ bool team_barrier(const TeamSync &ts, uint32_t team, uint32_t target,
+                                             uint32_t *sh_ok) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's reservations / zeroing done
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t *ctr = ts.arrive + team * kTeamArriveStride;
+        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t t0 = wall_clock64();
+        uint32_t ok = 1;
+        while (ld_agent(ctr) < target) {
+            if (ld_agent(ts.abort)) {
+                ok = 0;
+                break;
+            }
+            if (wall_clock64() - t0 > kTeamTimeout) {
+                atomicOr(ts.abort, 1u);
+                atomicOr(ts.err, 8u);
+                ok = 0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        *sh_ok = ok;
+    }
+    __syncthreads();
+    return *sh_ok != 0;
+}
+
+// Level 2 over S level-1 buckets (seg_start / seg_cnt; every count <= T *
+// kTeamSub, checked by the host): records of bucket s land in out[seg_start[s],
+// + seg_cnt[s]) grouped by digit (F2 <= kTeamF digits; the scans run over
+// kTeamF, the digits past F2 count 0); base_out[s][d] / tot_out[s][d] = start
+// and count of fine bucket (s, d), d < F2.  gridDim.x = 8 T workgroups, all
+// resident.
+template <class R>
+__global__ __launch_bounds__(kScatThreads) void k_part2_team(SrcAoS<R> src,
+                                                             const int64_t *seg_start,
+                                                             const uint32_t *seg_cnt, uint32_t S,
+                                                             uint32_t F2, R *out, int64_t *base_out,
+                                                             uint32_t *tot_out, TeamSync ts) {
+    constexpr int IPT = kTeamIPT;
+    constexpr int SUB = kTeamSub;
+    constexpr uint32_t F = kTeamF;
+    constexpr int DPT = F / kScatThreads;  // digits per thread in the scans
+    using W = Words<R>;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    W *stage = reinterpret_cast<W *>(smem);  // [SUB + 1]: slot SUB takes the padding
+    uint32_t *cnt = reinterpret_cast<uint32_t *>(smem + sizeof(R) * (SUB + 1));
+    uint32_t *dstart = cnt + F;     // [F + 1] local digit starts
+    uint32_t *cur = dstart + F + 1; // [F] this member's run start inside the bucket
+    uint32_t *sh16 = cur + F;       // [16] wave totals
+    __shared__ uint32_t sh_ok;
+    const uint32_t team = blockIdx.x & 7u;
+    const uint32_t T = gridDim.x >> 3;
+    const uint32_t m = blockIdx.x >> 3;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wv = tid >> 6;
+    for (uint32_t d = tid; d < F; d += kScatThreads) cnt[d] = 0;
+    __syncthreads();
+    // element j of a thread: 16-byte pair loads, as k_scatter's pair sources
+    auto elem = [tid](int j) -> uint32_t {
+        return (uint32_t)((j >> 1) * 2 * kScatThreads + 2 * tid + (j & 1));
+    };
+    uint32_t k = 0;  // buckets done = team barriers passed
+    for (uint32_t s = team; s < S; s += 8) {
+        const uint32_t n = __builtin_amdgcn_readfirstlane(seg_cnt[s]);
+        const int64_t st0 = seg_start[s];
+        const int64_t st = (int64_t)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)st0 >> 32)) << 32) |
+                                     (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)st0));
+        if (n == 0) {
+            if (m == 0)
+                for (uint32_t d = tid; d < F2; d += kScatThreads) {
+                    base_out[(size_t)s * F2 + d] = st;
+                    tot_out[(size_t)s * F2 + d] = 0;
+                }
+            continue;  // uniform over the team: no barrier
+        }
+        const uint32_t q = (n + T - 1) / T;
+        const uint32_t b0 = min(n, m * q);
+        const uint32_t lim = min(n, b0 + q) - b0;  // <= SUB (host check)
+        uint32_t *tt = ts.tot + ((size_t)team * 3 + k % 3) * F;
+        // ---- load + rank (one LDS atomic per record)
+        R rec[IPT];
+        uint32_t dr[IPT];
+        if (lim >= 2) {
+#pragma unroll
+            for (int mm = 0; mm < IPT / 2; ++mm) {
+                const uint32_t o = mm * 2 * kScatThreads + 2 * tid;
+                const uint32_t a = min(o, lim - 2);
+                R x0, x1;
+                src.fetch2(st + b0 + a, x0, x1);
+                rec[2 * mm] = a == o ? x0 : x1;
+                rec[2 * mm + 1] = x1;
+            }
+        } else {
+            // one record (or none: a member past the bucket's end loads nothing)
+#pragma unroll
+            for (int j = 0; j < IPT; ++j) rec[j] = lim ? src.fetch(st + b0) : R{};
+        }
+        {
+            uint32_t dg[IPT];
+            bool okv[IPT];
+#pragma unroll
+            for (int j = 0; j < IPT; ++j) {
+                okv[j] = elem(j) < lim;
+                dg[j] = okv[j] ? src.digit(rec[j]) : 0u;
+            }
+            uint32_t rk[IPT];
+#pragma unroll
+            for (int j = 0; j < IPT; ++j) rk[j] = atomicAdd(&cnt[dg[j]], okv[j] ? 1u : 0u);
+#pragma unroll
+            for (int j = 0; j < IPT; ++j) dr[j] = okv[j] ? (dg[j] | (rk[j] << 12)) : ~0u;
+        }
+        __syncthreads();
+        // ---- local digit starts; runs reserved in the team totals
+        {
+            const uint32_t d0 = DPT * tid;
+            uint32_t c[DPT], x = 0;
+#pragma unroll
+            for (int u = 0; u < DPT; ++u) {
+                c[u] = cnt[d0 + u];
+                x += c[u];
+            }
+            uint32_t wt;
+            uint32_t e = wave_excl_scan(x, wt);
+            if (lane == 63) sh16[wv] = wt;
+            __syncthreads();
+#pragma unroll
+            for (int w = 0; w < kScatThreads / 64; ++w)
+                if (w < wv) e += sh16[w];
+#pragma unroll
+            for (int u = 0; u < DPT; ++u) {
+                dstart[d0 + u] = e;
+                cur[d0 + u] = c[u] ? atomicAdd(&tt[d0 + u], c[u]) : 0u;
+                cnt[d0 + u] = 0;
+                e += c[u];
+            }
+            if (tid == 0) dstart[F] = lim;
+        }
+        ++k;
+        if (!team_barrier(ts, team, T * k, &sh_ok)) return;
+        // ---- the bucket's digit starts from the team totals
+        {
+            const uint32_t d0 = DPT * tid;
+            uint32_t c[DPT], x = 0;
+#pragma unroll
+            for (int u = 0; u < DPT; ++u) {
+                c[u] = ld_agent(&tt[d0 + u]);
+                x += c[u];
+            }
+            uint32_t wt;
+            uint32_t e = wave_excl_scan(x, wt);
+            if (lane == 63) sh16[wv] = wt;
+            __syncthreads();
+#pragma unroll
+            for (int w = 0; w < kScatThreads / 64; ++w)
+                if (w < wv) e += sh16[w];
+            uint32_t *tz = ts.tot + ((size_t)team * 3 + (k + 1) % 3) * F;  // the bucket after next
+#pragma unroll
+            for (int u = 0; u < DPT; ++u) {
+                cur[d0 + u] += e;
+                if (m == 0) {
+                    if (d0 + u < F2) {
+                        base_out[(size_t)s * F2 + d0 + u] = st + e;
+                        tot_out[(size_t)s * F2 + d0 + u] = c[u];
+                    }
+                    __hip_atomic_store(&tz[d0 + u], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                e += c[u];
+            }
+        }
+        // ---- stage by local digit, write every digit's run contiguously
+#pragma unroll
+        for (int j = 0; j < IPT; ++j) {
+            const uint32_t pos = dr[j] != ~0u ? dstart[dr[j] & 0xFFFu] + (dr[j] >> 12) : (uint32_t)SUB;
+            stage[pos] = to_words(rec[j]);
+        }
+        __syncthreads();
+        constexpr int WB = 4;
+        for (uint32_t k0 = 0; k0 < lim; k0 += WB * kScatThreads) {
+            W x[WB];
+            uint32_t dd[WB], kc[WB];
+#pragma unroll
+            for (int u = 0; u < WB; ++u) {
+                kc[u] = min(k0 + u * kScatThreads + tid, lim - 1);
+                x[u] = stage[kc[u]];
+                dd[u] = src.digit(from_words<R>(x[u]));
+            }
+            uint32_t c1[WB], c2[WB];
+#pragma unroll
+            for (int u = 0; u < WB; ++u) {
+                c1[u] = cur[dd[u]];
+                c2[u] = dstart[dd[u]];
+            }
+#pragma unroll
+            for (int u = 0; u < WB; ++u)
+                *reinterpret_cast<W *>(&out[st + c1[u] + (kc[u] - c2[u])]) = x[u];
+        }
+        __syncthreads();  // dstart / cur / stage are rewritten by the next bucket
+    }
+}
+
+}  // namespace dpg

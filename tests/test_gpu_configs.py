@@ -93,6 +93,27 @@ def test_config2_bounding_triggered_matches_oracle(built, config2_data):
     assert np.allclose(out.values.cpu().numpy()[np.argsort(gid)], o[ids], rtol=1e-12, atol=1e-6)
 
 
+@pytest.mark.parametrize("mode", ["team", "grouped", "team_abort"])
+def test_config2_level2_paths_match_oracle(built, config2_data, monkeypatch, mode):
+    """Level 2 three ways, every one bit-exact against the oracle (kept pairs,
+    counts; sums to 1e-9): the team kernel without a histogram pass
+    (dpg_team.h, the default for 8-byte records), the grouped histogram path
+    (DPG_TEAM_L2=0), and a team whose barrier gives up (test hook
+    DPG_DEBUG_TEAM_ABORT: abort flag + err bit 8, as after a timeout), which
+    the host detects at the chunking sync and redoes with the histogram path."""
+    if mode == "grouped":
+        monkeypatch.setenv("DPG_TEAM_L2", "0")
+    if mode == "team_abort":
+        monkeypatch.setenv("DPG_DEBUG_TEAM_ABORT", "1")
+    pid, pk, val = config2_data
+    res, _, got = _run(pid, pk, val, _c2_params(8, 2), P2)
+    ref = oracle.bound_aggregate(pid, pk, val, res.last_bound_fields, SEED)
+    _assert_partials(got, ref)
+    stages = res.backend.ctx.stage_times()
+    assert ("partition2:team" in stages) == (mode != "grouped")
+    assert ("partition2:hist" in stages) == (mode != "team")
+
+
 # ------------------------------------------------------------------ config 4
 N4, U4, P4 = 20_000_000, 100_000, 100_000_000
 
