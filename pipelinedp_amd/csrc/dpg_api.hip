@@ -1125,7 +1125,8 @@ int pipeline(dpg_ctx *ctx, hipStream_t s, const int64_t *pid, const int64_t *pk,
     const uint32_t team_T = (uint32_t)ctx->n_cu / 8;
     bool team = sizeof(R) == 8 && pl.b2 >= 6 && pl.b2 <= kMaxB1 && ctx->n_cu % 8 == 0 && team_T > 0 && l1_grp &&
                 env_int("DPG_TEAM_L2", 1) != 0;
-    if (team) {
+    if constexpr (sizeof(R) != 8) team = false;
+    if constexpr (sizeof(R) == 8) if (team) {
         int occ = 0;
         const void *tk = (const void *)k_part2_team<R>;
         (void)hipFuncSetAttribute(tk, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1181,10 +1182,13 @@ int pipeline(dpg_ctx *ctx, hipStream_t s, const int64_t *pid, const int64_t *pk,
     };
     if (pl.b2 > 0) {
         const uint32_t F2 = 1u << pl.b2;
-        if (team) {
-            SrcAoS<R> s2{recA, f, shift2, F2 - 1};
-            r = run_team_level2<R>(ctx, s, s2, F1, F2, bstart1, bcnt1, recB, ctl, &bstart, &bcnt);
-        } else {
+        if constexpr (sizeof(R) == 8) {
+            if (team) {
+                SrcAoS<R> s2{recA, f, shift2, F2 - 1};
+                r = run_team_level2<R>(ctx, s, s2, F1, F2, bstart1, bcnt1, recB, ctl, &bstart, &bcnt);
+            }
+        }
+        if (!team) {
             r = level2_grouped();
         }
         if (r) return r;

@@ -127,42 +127,55 @@ __global__ __launch_bounds__(kScatThreads) void k_part2_team(SrcAoS<R> src,
     auto elem = [tid](int j) -> uint32_t {
         return (uint32_t)((j >> 1) * 2 * kScatThreads + 2 * tid + (j & 1));
     };
-    uint32_t k = 0;  // buckets done = team barriers passed
-    for (uint32_t s = team; s < S; s += 8) {
-        const uint32_t n = __builtin_amdgcn_readfirstlane(seg_cnt[s]);
+    // this member's share of bucket s: [st + b0, + lim)
+    auto share = [&](uint32_t s, int64_t &st, uint32_t &n, uint32_t &b0, uint32_t &lim) {
+        n = __builtin_amdgcn_readfirstlane(seg_cnt[s]);
         const int64_t st0 = seg_start[s];
-        const int64_t st = (int64_t)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)st0 >> 32)) << 32) |
-                                     (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)st0));
-        if (n == 0) {
-            if (m == 0)
-                for (uint32_t d = tid; d < F2; d += kScatThreads) {
-                    base_out[(size_t)s * F2 + d] = st;
-                    tot_out[(size_t)s * F2 + d] = 0;
-                }
-            continue;  // uniform over the team: no barrier
-        }
+        st = (int64_t)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)st0 >> 32)) << 32) |
+                       (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)st0));
         const uint32_t q = (n + T - 1) / T;
-        const uint32_t b0 = min(n, m * q);
-        const uint32_t lim = min(n, b0 + q) - b0;  // <= SUB (host check)
-        uint32_t *tt = ts.tot + ((size_t)team * 3 + k % 3) * F;
-        // ---- load + rank (one LDS atomic per record)
-        R rec[IPT];
-        uint32_t dr[IPT];
+        b0 = min(n, m * q);
+        lim = min(n, b0 + q) - b0;  // <= SUB (host check)
+    };
+    R rec[IPT];
+    // loads of a share (unconditional, clamped into it: a guarded load would
+    // serialise them); a member past the bucket's end loads nothing
+    auto load = [&](int64_t base, uint32_t lim) {
         if (lim >= 2) {
 #pragma unroll
             for (int mm = 0; mm < IPT / 2; ++mm) {
                 const uint32_t o = mm * 2 * kScatThreads + 2 * tid;
                 const uint32_t a = min(o, lim - 2);
                 R x0, x1;
-                src.fetch2(st + b0 + a, x0, x1);
+                src.fetch2(base + a, x0, x1);
                 rec[2 * mm] = a == o ? x0 : x1;
                 rec[2 * mm + 1] = x1;
             }
         } else {
-            // one record (or none: a member past the bucket's end loads nothing)
 #pragma unroll
-            for (int j = 0; j < IPT; ++j) rec[j] = lim ? src.fetch(st + b0) : R{};
+            for (int j = 0; j < IPT; ++j) rec[j] = lim ? src.fetch(base) : R{};
         }
+    };
+    uint32_t k = 0;      // buckets done = team barriers passed
+    bool have = false;   // rec[] holds this member's share of bucket s (prefetched)
+    for (uint32_t s = team; s < S; s += 8) {
+        int64_t st;
+        uint32_t n, b0, lim;
+        share(s, st, n, b0, lim);
+        if (n == 0) {
+            if (m == 0)
+                for (uint32_t d = tid; d < F2; d += kScatThreads) {
+                    base_out[(size_t)s * F2 + d] = st;
+                    tot_out[(size_t)s * F2 + d] = 0;
+                }
+            have = false;
+            continue;  // uniform over the team: no barrier
+        }
+        uint32_t *tt = ts.tot + ((size_t)team * 3 + k % 3) * F;
+        // ---- load (unless prefetched during the last write-out) + rank
+        if (!have) load(st + b0, lim);
+        have = false;
+        uint32_t dr[IPT];
         {
             uint32_t dg[IPT];
             bool okv[IPT];
@@ -242,6 +255,16 @@ __global__ __launch_bounds__(kScatThreads) void k_part2_team(SrcAoS<R> src,
             stage[pos] = to_words(rec[j]);
         }
         __syncthreads();
+        // ---- the next bucket's share loads while this one is written out
+        if (s + 8 < S) {
+            int64_t st2;
+            uint32_t n2, b02, lim2;
+            share(s + 8, st2, n2, b02, lim2);
+            if (n2 > 0) {
+                load(st2 + b02, lim2);
+                have = true;
+            }
+        }
         constexpr int WB = 4;
         for (uint32_t k0 = 0; k0 < lim; k0 += WB * kScatThreads) {
             W x[WB];
