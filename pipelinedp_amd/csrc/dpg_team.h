@@ -156,8 +156,7 @@ __global__ __launch_bounds__(kScatThreads) void k_part2_team(SrcAoS<R> src,
             for (int j = 0; j < IPT; ++j) rec[j] = lim ? src.fetch(base) : R{};
         }
     };
-    uint32_t k = 0;      // buckets done = team barriers passed
-    bool have = false;   // rec[] holds this member's share of bucket s (prefetched)
+    uint32_t k = 0;  // buckets done = team barriers passed
     for (uint32_t s = team; s < S; s += 8) {
         int64_t st;
         uint32_t n, b0, lim;
@@ -168,13 +167,11 @@ __global__ __launch_bounds__(kScatThreads) void k_part2_team(SrcAoS<R> src,
                     base_out[(size_t)s * F2 + d] = st;
                     tot_out[(size_t)s * F2 + d] = 0;
                 }
-            have = false;
             continue;  // uniform over the team: no barrier
         }
         uint32_t *tt = ts.tot + ((size_t)team * 3 + k % 3) * F;
-        // ---- load (unless prefetched during the last write-out) + rank
-        if (!have) load(st + b0, lim);
-        have = false;
+        // ---- load + rank
+        load(st + b0, lim);
         uint32_t dr[IPT];
         {
             uint32_t dg[IPT];
@@ -255,16 +252,8 @@ __global__ __launch_bounds__(kScatThreads) void k_part2_team(SrcAoS<R> src,
             stage[pos] = to_words(rec[j]);
         }
         __syncthreads();
-        // ---- the next bucket's share loads while this one is written out
-        if (s + 8 < S) {
-            int64_t st2;
-            uint32_t n2, b02, lim2;
-            share(s + 8, st2, n2, b02, lim2);
-            if (n2 > 0) {
-                load(st2 + b02, lim2);
-                have = true;
-            }
-        }
+        // (loading the next bucket's share during the write-out measured
+        // slower: 5.2 -> 5.65 ms at config 2, 128 VGPRs with spills)
         constexpr int WB = 4;
         for (uint32_t k0 = 0; k0 < lim; k0 += WB * kScatThreads) {
             W x[WB];
