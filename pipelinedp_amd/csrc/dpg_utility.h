@@ -113,10 +113,19 @@ __global__ __launch_bounds__(64) void k_ua_accumulate(const ItemPA *pairs,
     // PRIVACY_ID_COUNT's (x = 1 for count > 0) follow from the moments at the
     // flush: total rn - nz, l0 terms -(sum of 1 - p) = e - rn and sum of q =
     // v, corrected by the pairs of count 0 (pre-aggregated input only).
-    double e = 0, v = 0, t = 0, rn = 0, rc = 0;
+    // FP64 arithmetic is what bounds this loop (half the FP32 vector rate;
+    // config 5: ~7e8 pairs x 64 configurations), so the integer terms stay
+    // integers (pairs and records per partition, COUNT's clip-to-max error)
+    // and the float ones use min / max / fma forms (same values, fewer
+    // instructions than compare-and-select chains).
+    double e = 0, v = 0, t = 0;
+    uint32_t rn = 0;                   // pairs of the partition (wave-uniform)
+    uint64_t rc = 0;                   // records of the partition (wave-uniform)
     ErrAcc es;
-    double cmx = 0, cel = 0, cvl = 0;  // COUNT: clip-to-max, l0 mean, l0 variance
+    int64_t cmx = 0;                   // COUNT: clip-to-max error (integer)
+    double cel = 0, cvl = 0;           // COUNT: l0 mean, l0 variance
     double nz = 0, zel = 0, zvl = 0;   // pairs of count 0: number, sum 1 - p, sum q
+    const uint32_t mcpp_i = cf.mcpp >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)cf.mcpp;
     es.clear();
     uint32_t cur = pairs[lo].pk;
     bool skip = a.sample_mask && !bit_of(a.sample_mask, cur);
@@ -124,9 +133,10 @@ __global__ __launch_bounds__(64) void k_ua_accumulate(const ItemPA *pairs,
         if (skip) return;
         const bool atomic = !(pstart[pk] >= lo && pstart[pk + 1] <= hi);
         const int64_t C64 = C;
+        const double rnd = (double)rn, rcd = (double)rc;
         if (c == 0) {
-            ua_put(&a.raw[2 * (int64_t)pk], rn, atomic);
-            ua_put(&a.raw[2 * (int64_t)pk + 1], rc, atomic);
+            ua_put(&a.raw[2 * (int64_t)pk], rnd, atomic);
+            ua_put(&a.raw[2 * (int64_t)pk + 1], rcd, atomic);
         }
         if (!lane_on) return;
         double *m = a.mom + (int64_t)pk * kUaMom * C64 + c;
@@ -143,8 +153,8 @@ __global__ __launch_bounds__(64) void k_ua_accumulate(const ItemPA *pairs,
             o += 5 * C64;
         };
         if (a.has_sum) put5(es.tot, es.cmin, es.cmax, es.el0, es.vl0);
-        if (a.has_count) put5(rc, 0.0, cmx, cel, cvl);
-        if (a.has_pid) put5(rn - nz, 0.0, 0.0, (e - rn) + zel, v - zvl);
+        if (a.has_count) put5(rcd, 0.0, (double)cmx, cel, cvl);
+        if (a.has_pid) put5(rnd - nz, 0.0, 0.0, (e - rnd) + zel, v - zvl);
     };
     for (int64_t b = lo; b < hi; b += 64) {
         const int64_t i = b + c < hi ? b + c : hi - 1;
@@ -158,9 +168,12 @@ __global__ __launch_bounds__(64) void k_ua_accumulate(const ItemPA *pairs,
             const uint32_t pk = __builtin_amdgcn_readlane(mine.pk, j);
             if (pk != cur) {
                 flush(cur);
-                e = v = t = rn = rc = 0.0;
+                e = v = t = 0.0;
+                rn = 0;
+                rc = 0;
                 es.clear();
-                cmx = cel = cvl = 0.0;
+                cmx = 0;
+                cel = cvl = 0.0;
                 nz = zel = zvl = 0.0;
                 cur = pk;
                 skip = a.sample_mask && !bit_of(a.sample_mask, cur);
@@ -176,29 +189,28 @@ __global__ __launch_bounds__(64) void k_ua_accumulate(const ItemPA *pairs,
             const double q = p * omp;
             e += p;
             v += q;
-            t += q * (1.0 - 2.0 * p);
-            rn += 1.0;
-            rc += (double)cnt;
+            t = fma(q, fma(-2.0, p, 1.0), t);
+            rn += 1;
+            rc += cnt;
             if (a.has_sum) {
                 const uint32_t slo =
                     __builtin_amdgcn_readlane((uint32_t)__double_as_longlong(mine.sum), j);
                 const uint32_t shi =
                     __builtin_amdgcn_readlane((uint32_t)(__double_as_longlong(mine.sum) >> 32), j);
                 const double x = __longlong_as_double((long long)(((uint64_t)shi << 32) | slo));
-                const double pc = x < cf.lo ? cf.lo : (x > cf.hi ? cf.hi : x);
-                const double d = pc - x;
+                const double pc = fmin(fmax(x, cf.lo), cf.hi);
                 es.tot += x;
-                es.cmin += x < cf.lo ? d : 0.0;
-                es.cmax += x > cf.hi ? d : 0.0;
-                es.el0 -= pc * omp;
-                es.vl0 += pc * pc * q;
+                es.cmin += fmax(cf.lo - x, 0.0);  // pc - x where x < lo
+                es.cmax += fmin(cf.hi - x, 0.0);  // pc - x where x > hi
+                es.el0 = fma(-pc, omp, es.el0);
+                es.vl0 = fma(pc * pc, q, es.vl0);
             }
             if (a.has_count) {
-                const double x = (double)cnt;
-                const double pc = x > cf.mcpp ? cf.mcpp : x;
-                cmx += pc - x;
-                cel -= pc * omp;
-                cvl += pc * pc * q;
+                const uint32_t pci = cnt < mcpp_i ? cnt : mcpp_i;
+                const double pc = (double)pci;
+                cmx += (int64_t)pci - (int64_t)cnt;
+                cel = fma(-pc, omp, cel);
+                cvl = fma(pc * pc, q, cvl);
             }
             if (a.has_pid && cnt == 0) {  // wave-uniform (the pair is broadcast)
                 nz += 1.0;
