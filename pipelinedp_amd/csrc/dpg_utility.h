@@ -129,9 +129,16 @@ __global__ __launch_bounds__(64) void k_ua_accumulate(const ItemPA *pairs,
     es.clear();
     uint32_t cur = pairs[lo].pk;
     bool skip = a.sample_mask && !bit_of(a.sample_mask, cur);
+    // only the run's first and last partitions can be split with the
+    // neighbouring runs (added atomically); decided here, so that a flush
+    // loads nothing (a load in the flush waited for the previous flush's
+    // stores)
+    const uint32_t pk_first = pairs[lo].pk, pk_last = pairs[hi - 1].pk;
+    const bool split_first = lo > 0 && pairs[lo - 1].pk == pk_first;
+    const bool split_last = hi < n && pairs[hi].pk == pk_last;
     auto flush = [&](uint32_t pk) {
         if (skip) return;
-        const bool atomic = !(pstart[pk] >= lo && pstart[pk + 1] <= hi);
+        const bool atomic = (pk == pk_first && split_first) || (pk == pk_last && split_last);
         const int64_t C64 = C;
         const double rnd = (double)rn, rcd = (double)rc;
         if (c == 0) {
@@ -156,16 +163,26 @@ __global__ __launch_bounds__(64) void k_ua_accumulate(const ItemPA *pairs,
         if (a.has_count) put5(rcd, 0.0, (double)cmx, cel, cvl);
         if (a.has_pid) put5(rnd - nz, 0.0, 0.0, (e - rnd) + zel, v - zvl);
     };
+    // The 64 pairs of a block are broadcast to the configurations through
+    // LDS (uniform-address reads), not by readlane of the loaded registers:
+    // with the loaded registers live in the loop, every iteration waited for
+    // all vector memory operations (s_waitcnt vmcnt(0) at the loop head),
+    // i.e. for the stores of every partition flush.
+    __shared__ uint32_t s_pk[64], s_cnt[64];
+    __shared__ double s_sum[64], s_inv[64];
     for (int64_t b = lo; b < hi; b += 64) {
         const int64_t i = b + c < hi ? b + c : hi - 1;
         const ItemPA mine = pairs[i];
-        // 1 / n_partitions of the lane's pair, broadcast below: one division
-        // per pair instead of one per (pair, configuration)
-        const double inv_mine = mine.npart > 0 ? 1.0 / (double)mine.npart : 0.0;
-        const long long inv_bits = __double_as_longlong(inv_mine);
+        // 1 / n_partitions of the lane's pair: one division per pair instead
+        // of one per (pair, configuration)
+        s_pk[c] = mine.pk;
+        s_cnt[c] = mine.cnt;
+        s_sum[c] = mine.sum;
+        s_inv[c] = mine.npart > 0 ? 1.0 / (double)mine.npart : 0.0;
+        __syncthreads();
         const int m = (int)(hi - b < 64 ? hi - b : 64);
         for (int j = 0; j < m; ++j) {
-            const uint32_t pk = __builtin_amdgcn_readlane(mine.pk, j);
+            const uint32_t pk = __builtin_amdgcn_readfirstlane(s_pk[j]);
             if (pk != cur) {
                 flush(cur);
                 e = v = t = 0.0;
@@ -179,10 +196,8 @@ __global__ __launch_bounds__(64) void k_ua_accumulate(const ItemPA *pairs,
                 skip = a.sample_mask && !bit_of(a.sample_mask, cur);
             }
             if (skip) continue;
-            const uint32_t cnt = __builtin_amdgcn_readlane(mine.cnt, j);
-            const uint32_t ilo = __builtin_amdgcn_readlane((uint32_t)inv_bits, j);
-            const uint32_t ihi = __builtin_amdgcn_readlane((uint32_t)(inv_bits >> 32), j);
-            const double inv = __longlong_as_double((long long)(((uint64_t)ihi << 32) | ilo));
+            const uint32_t cnt = __builtin_amdgcn_readfirstlane(s_cnt[j]);
+            const double inv = s_inv[j];
             // l0 keep probability of this pair (per_partition_combiners.py:203-205)
             const double p = fmin(1.0, cf.mpc * inv);
             const double omp = 1.0 - p;
@@ -193,11 +208,7 @@ __global__ __launch_bounds__(64) void k_ua_accumulate(const ItemPA *pairs,
             rn += 1;
             rc += cnt;
             if (a.has_sum) {
-                const uint32_t slo =
-                    __builtin_amdgcn_readlane((uint32_t)__double_as_longlong(mine.sum), j);
-                const uint32_t shi =
-                    __builtin_amdgcn_readlane((uint32_t)(__double_as_longlong(mine.sum) >> 32), j);
-                const double x = __longlong_as_double((long long)(((uint64_t)shi << 32) | slo));
+                const double x = s_sum[j];
                 const double pc = fmin(fmax(x, cf.lo), cf.hi);
                 es.tot += x;
                 es.cmin += fmax(cf.lo - x, 0.0);  // pc - x where x < lo
@@ -218,6 +229,7 @@ __global__ __launch_bounds__(64) void k_ua_accumulate(const ItemPA *pairs,
                 zvl += q;
             }
         }
+        __syncthreads();  // the next block rewrites s_*
     }
     flush(cur);
 }
