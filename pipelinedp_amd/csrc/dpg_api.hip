@@ -1773,9 +1773,16 @@ int dpg_utility_analysis(dpg_ctx *ctx, const dpg_pair_entry *pairs,
         stage(ctx, s, "ua.select");
         const unsigned g = (unsigned)std::min<int64_t>(P, (int64_t)ctx->n_cu * 16);
         const size_t lds = (size_t)a.npi * a.n_cls * 8;
-        (void)hipFuncSetAttribute((const void *)k_ua_select,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        k_ua_select<<<g, 64, lds, s>>>(reinterpret_cast<const ItemPA *>(pairs), partition_start, a);
+        // lanes per selection class of the exact PMF (dpg_utility.h)
+        auto launch = [&](auto kern) {
+            (void)hipFuncSetAttribute((const void *)kern,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            kern<<<g, 64, lds, s>>>(reinterpret_cast<const ItemPA *>(pairs), partition_start, a);
+        };
+        if (a.n_cls <= 8) launch(k_ua_select<8>);
+        else if (a.n_cls <= 16) launch(k_ua_select<4>);
+        else if (a.n_cls <= 32) launch(k_ua_select<2>);
+        else launch(k_ua_select<1>);
         LAUNCH_CHECK();
     }
     if (report) {

@@ -302,9 +302,22 @@ __device__ __forceinline__ void ua_pi_range(const UaConfig &cf, int64_t &i0, int
 // LDS once per wave ([i][class]): the dot products below read it instead of
 // one dependent global table load per count (those loads bounded the
 // kernel: 61 ms for 64 configurations over 1e6 partitions).
+//
+// LPC > 1 (at most 64 / LPC selection classes): the exact PMF depends on the
+// class only (p = min(1, l0 / n_partitions)), so the wave computes one PMF
+// per class, not per configuration: lane (class k, block l) holds
+// coefficients [l CPL, (l + 1) CPL) of class k's PMF (the carry from the
+// block below by one lane shuffle per pair), the dot with pi is summed over
+// the class's LPC lanes and every configuration lane reads its class's
+// value.  (Per configuration, the 104 coefficients held 208 VGPRs, one wave
+// per SIMD.)
+template <int LPC>
 __global__ __launch_bounds__(64) void k_ua_select(const ItemPA *pairs, const int64_t *pstart,
                                                   UaArgs a) {
     extern __shared__ __attribute__((aligned(16))) double spi[];
+    constexpr int NCO = kPgfB * kPgfNB;
+    constexpr int CPL = (NCO + LPC - 1) / LPC;
+    __shared__ double s_inv[kUaMaxExact + 28];
     const int c = (int)__lane_id();
     const int64_t C64 = a.n_configs;
     const bool lane_on = c < a.n_configs;
@@ -323,7 +336,42 @@ __global__ __launch_bounds__(64) void k_ua_select(const ItemPA *pairs, const int
         const int64_t b = pstart[k], n = pstart[k + 1] - b;
         if (n == 0 || (a.sample_mask && !bit_of(a.sample_mask, k))) continue;
         double keep = 0.0;
-        if (n <= kUaMaxExact) {
+        if constexpr (LPC > 1) if (n <= kUaMaxExact) {
+            const int kc = c / LPC, l = c % LPC;
+            const int kcs = kc < K ? kc : 0;
+            const double mpc_k = a.cfg[a.cls_rep[kcs]].mpc;
+            for (int x = c; x < n; x += 64) {
+                const uint32_t np = pairs[b + x].npart;
+                s_inv[x] = np > 0 ? 1.0 / (double)np : 0.0;
+            }
+            __syncthreads();
+            double co[CPL];
+#pragma unroll
+            for (int t = 0; t < CPL; ++t) co[t] = (l == 0 && t == 0) ? 1.0 : 0.0;
+            for (int64_t j = 0; j < n; ++j) {
+                const double inv = s_inv[j];
+                const double p = fmin(1.0, mpc_k * inv);
+                const double q = 1.0 - p;
+                double below = __shfl_up(co[CPL - 1], 1, 64);
+                below = l == 0 ? 0.0 : below;
+#pragma unroll
+                for (int t = CPL - 1; t >= 1; --t) co[t] = co[t] * q + co[t - 1] * p;
+                co[0] = co[0] * q + below * p;
+            }
+            double part = 0.0;
+#pragma unroll
+            for (int t = 0; t < CPL; ++t) {
+                const int i = l * CPL + t;
+                if (i <= n) part += co[t] * spi[i * K + kcs];
+            }
+#pragma unroll
+            for (int o = LPC / 2; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+            keep = __shfl(part, (my_sel >= 0 ? my_sel : 0) * LPC, 64);
+            __syncthreads();  // s_inv is rewritten by the next partition
+            if (lane_on) a.keep[k * C64 + c] = keep;
+            continue;
+        }
+        if (LPC == 1 && n <= kUaMaxExact) {
             // 1 / n_partitions of pairs lane and lane + 64, broadcast below
             const uint32_t n0 = pairs[b + min((int64_t)c, n - 1)].npart;
             const uint32_t n1 = pairs[b + min((int64_t)c + 64, n - 1)].npart;
