@@ -472,16 +472,16 @@ struct Ipt {
 #ifndef DPG_IPT_L1
 #define DPG_IPT_L1 11  // same-box A/B config 2: 12 -> 11 level-1 scatter 7.88 -> 7.25 ms (spills)
 #endif
-    static constexpr int L1 = sizeof(R) == 8 ? DPG_IPT_L1 : 8;
+    static constexpr int L1 = sizeof(R) == 8 ? DPG_IPT_L1 : sizeof(R) == 16 ? 7 : 8;
 #ifndef DPG_IPT_LN
 #define DPG_IPT_LN 12  // same-box A/B config 2: 16 -> 12 level-2 scatter 5.97 -> 4.37 ms (spills)
 #endif
-    static constexpr int LN = sizeof(R) == 8 ? DPG_IPT_LN : 10;
+    static constexpr int LN = sizeof(R) == 8 ? DPG_IPT_LN : sizeof(R) == 16 ? 8 : 10;
     // the refine level has few digits (wave-aggregated ranking, which holds
     // more registers per record: at LN records per thread it spilled)
     static constexpr int LR = sizeof(R) == 8 ? 8 : 6;
     // level 2 with 4096 digits: the digit arrays take 48 KB of LDS
-    static constexpr int LW = sizeof(R) == 8 ? 12 : 8;
+    static constexpr int LW = sizeof(R) == 8 ? 12 : sizeof(R) == 16 ? 6 : 8;
 };
 
 BoundParams to_bound(const dpg_bound_params *p, uint64_t seed) {

@@ -460,7 +460,7 @@ __global__ __launch_bounds__(kBigThreads) void k_bound_big(
                 const uint32_t st = pairst[p];
                 if (st == kDropped) continue;
                 if (st != kKeptAll && rkey[i] > pool[st + bp.mcpp - 1]) continue;
-                const double v = bp.value[RecOps<R>::idx(rb[i], f)];
+                const double v = rec_value<R>(rb[i], bp.value, f);
                 if (part_clip) {
                     atomicAdd(&acc_sum[p], v);
                 } else {
@@ -495,7 +495,7 @@ __global__ __launch_bounds__(kBigThreads) void k_bound_big(
             const uint32_t p = rps[i];
             atomicAdd(&pairst[p], 1u);
             if (need_v) {
-                const double v = bp.value[RecOps<R>::idx(rb[i], f)];
+                const double v = rec_value<R>(rb[i], bp.value, f);
                 if (part_clip) {
                     atomicAdd(&acc_sum[p], v);
                 } else {

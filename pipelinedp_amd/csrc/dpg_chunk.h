@@ -402,7 +402,7 @@ __device__ __forceinline__ void bound_chunk(const R (&r)[kRPT], uint32_t n, uint
             // bits), so a sampled pair's base is the low 16 bits
             st[k] = valid[k] ? pairst[ps[k]] : kDropped;
             if (st[k] < kKeptAll) st[k] &= 0xFFFFu;
-            if (need_v && st[k] != kDropped) v[k] = bp.value[RecOps<R>::idx(r[k], f)];
+            if (need_v && st[k] != kDropped) v[k] = rec_value<R>(r[k], bp.value, f);
         }
         if (sample) {
 #pragma unroll
@@ -471,7 +471,7 @@ __device__ __forceinline__ void bound_chunk(const R (&r)[kRPT], uint32_t n, uint
             const uint32_t p = ps[k];
             atomicAdd(&pairst[p], 1u);
             if (need_v) {
-                const double v = bp.value[RecOps<R>::idx(r[k], f)];
+                const double v = rec_value<R>(r[k], bp.value, f);
                 if (part_clip) {
                     atomicAdd(&acc_sum[p], v);
                 } else {

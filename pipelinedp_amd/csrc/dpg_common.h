@@ -31,6 +31,14 @@ struct alignas(8) R8 {
 struct alignas(4) R12 {
     uint32_t lo, hi, idx;
 };
+//   R16: an R8 word and the record's value (the utility pre-aggregate, which
+//        sums the value of every record: carrying it through the partition
+//        levels moves 8 more bytes per record per pass where a gather by index
+//        would fetch a whole 128-byte line per record)
+struct alignas(16) R16 {
+    uint64_t w;
+    double v;
+};
 
 struct Fmt {
     uint32_t ib;      // R8: bits of the record index
@@ -54,6 +62,18 @@ struct RecOps<R8> {
     }
 };
 template <>
+struct RecOps<R16> {
+    static __host__ __device__ __forceinline__ uint64_t key(const R16 &r, const Fmt &f) {
+        return r.w >> f.ib;
+    }
+    static __host__ __device__ __forceinline__ uint32_t idx(const R16 &r, const Fmt &f) {
+        return (uint32_t)(r.w & ((1ull << f.ib) - 1ull));
+    }
+    static __host__ __device__ __forceinline__ R16 make(uint64_t key, uint32_t idx, const Fmt &f) {
+        return R16{(key << f.ib) | idx, 0.0};
+    }
+};
+template <>
 struct RecOps<R12> {
     static __host__ __device__ __forceinline__ uint64_t key(const R12 &r, const Fmt &) {
         return ((uint64_t)r.hi << 32) | r.lo;
@@ -65,6 +85,18 @@ struct RecOps<R12> {
         return R12{(uint32_t)key, (uint32_t)(key >> 32), idx};
     }
 };
+
+// The value of a record: carried in an R16, else gathered from the input
+// column by the record's index.
+template <class R>
+__device__ __forceinline__ double rec_value(const R &r, const double *value, const Fmt &f) {
+#if DPG_EXP_NO_GATHER  // experiment: what the gathers cost (values read as 0)
+    return 0.0;
+#else
+    if constexpr (sizeof(R) == 16) return r.v;
+    else return value[RecOps<R>::idx(r, f)];
+#endif
+}
 
 struct alignas(16) Item16 {  // one kept (pid, pk) pair: COUNT / SUM / PID
     uint32_t pk;

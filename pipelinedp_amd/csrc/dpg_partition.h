@@ -17,6 +17,8 @@
 
 #include "dpg_common.h"
 
+#include <type_traits>
+
 namespace dpg {
 
 #ifndef DPG_HIST_U
@@ -105,10 +107,18 @@ struct SrcSoAKey {
     // the stored key depend on (pid - pid_min) mod 2^32 alone, and the
     // histogram pass, which reads the whole column, raises the range error
     // (12 fewer VGPRs per thread in flight: the level-1 scatter spilled)
-    struct Raw {
+    // R16 records carry the value column too (the utility pre-aggregate)
+    static constexpr bool kV = sizeof(R) == 16;
+    struct RawK {
         uint32_t pid;
         int64_t pk;
     };
+    struct RawV {
+        uint32_t pid;
+        int64_t pk;
+        double v;
+    };
+    using Raw = std::conditional_t<kV, RawV, RawK>;
     const int64_t *pid;
     const int64_t *pk;
     const uint8_t *pub;  // public-partition bitmap or null
@@ -120,6 +130,7 @@ struct SrcSoAKey {
     uint64_t kmask;      // stored key bits
     uint32_t dshift;     // kbits - b1
     uint32_t *err;
+    const double *value = nullptr;  // R16 only
 #ifndef DPG_L1_NT
 #define DPG_L1_NT 1  // same-box A/B: level-1 scatter 8.15 -> 7.86 ms
 #endif
@@ -127,12 +138,19 @@ struct SrcSoAKey {
     // the key columns are read once: non-temporal loads leave L2 to the
     // scattered runs being written
     __device__ __forceinline__ Raw fetch(int64_t i) const {
-        return Raw{__builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(pid) + 2 * i),
-                   __builtin_nontemporal_load(pk + i)};
+        if constexpr (kV)
+            return Raw{__builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(pid) + 2 * i),
+                       __builtin_nontemporal_load(pk + i), __builtin_nontemporal_load(value + i)};
+        else
+            return Raw{__builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(pid) + 2 * i),
+                       __builtin_nontemporal_load(pk + i)};
     }
 #else
     __device__ __forceinline__ Raw fetch(int64_t i) const {
-        return Raw{reinterpret_cast<const uint32_t *>(pid)[2 * i], pk[i]};
+        if constexpr (kV)
+            return Raw{reinterpret_cast<const uint32_t *>(pid)[2 * i], pk[i], value[i]};
+        else
+            return Raw{reinterpret_cast<const uint32_t *>(pid)[2 * i], pk[i]};
     }
 #endif
     // keep decision shared by the histogram and the scatter (they must agree
@@ -149,6 +167,7 @@ struct SrcSoAKey {
         d = h >> dshift;
         const uint64_t key = (((uint64_t)h << f.pkbits) | (uint64_t)x.pk) & kmask;
         r = RecOps<R>::make(key, (uint32_t)i, f);
+        if constexpr (kV) r.v = x.v;
         return keep(a, x.pk);
     }
     // histogram view: the same digit and keep decision from pid (and pk

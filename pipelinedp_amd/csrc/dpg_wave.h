@@ -737,7 +737,7 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
             // (DPG_LATE_GATHER: most of them are not kept, and every gather
             // pulls a whole sector)
             if (need_v && (DPG_LATE_GATHER ? st[k] == kKeptAll : st[k] != kDropped))
-                v[k] = bp.value[RecOps<R>::idx(cur[k], f)];
+                v[k] = rec_value<R>(cur[k], bp.value, f);
         }
         if (sample) {
             uint32_t pv[kWRPT], pos[kWRPT];
@@ -782,7 +782,7 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
 #if DPG_LATE_GATHER
 #pragma unroll
                 for (int k = 0; k < kWRPT && k < (int)kn; ++k)
-                    if (st[k] < kKeptAll && rkey[k] <= thr[k]) v[k] = bp.value[RecOps<R>::idx(cur[k], f)];
+                    if (st[k] < kKeptAll && rkey[k] <= thr[k]) v[k] = rec_value<R>(cur[k], bp.value, f);
 #endif
             }
 #pragma unroll
@@ -853,7 +853,7 @@ bool overp[kWQPL];
         for (int k = 0; k < kWRPT && k < (int)kn; ++k) {
             v[k] = 0.0;
             if (((overm >> k) & 1u) && rkey[k] > thr[k]) validm &= ~(1u << k);
-            if (need_v && ((validm >> k) & 1u)) v[k] = bp.value[RecOps<R>::idx(cur[k], f)];
+            if (need_v && ((validm >> k) & 1u)) v[k] = rec_value<R>(cur[k], bp.value, f);
         }
 #pragma unroll
         for (int k = 0; k < kWRPT && k < (int)kn; ++k) {
