@@ -1085,6 +1085,7 @@ int pipeline(dpg_ctx *ctx, hipStream_t s, const int64_t *pid, const int64_t *pk,
     const uint32_t F1 = 1u << pl.b1;
     SrcSoAKey<R> s1{pid, pk, p->public_mask, pl.P, pid_min, U, H, f,
                     low_mask(pl.kbits - pl.b1 + pl.pkbits), pl.kbits - pl.b1, &ctl->err};
+    s1.value = value;  // read by R16 sources only
     int64_t *bstart = nullptr;
     uint32_t *bcnt = nullptr;
 #ifndef DPG_L1_XCD
@@ -1208,22 +1209,26 @@ int pipeline(dpg_ctx *ctx, hipStream_t s, const int64_t *pid, const int64_t *pk,
                                                                  n, out, ctl, pa)
                          : bound_and_reduce<R, uint64_t, ItemPA>(ctx, s, pl, cur, bstart, bcnt, B, bp,
                                                                  n, out, ctl, pa);
-        // MEAN / VARIANCE without SUM (and without per-partition sum clipping):
-        // 24-byte items with the normalised moments only
-        if (var && !(p->metric_mask & DPG_M_SUM) && p->sum_mode != DPG_SUM_CLIP_PARTITION)
-            return key32 ? bound_and_reduce<R, uint32_t, ItemV>(ctx, s, pl, cur, bstart, bcnt, B, bp,
-                                                                n, out, ctl, nullptr)
-                         : bound_and_reduce<R, uint64_t, ItemV>(ctx, s, pl, cur, bstart, bcnt, B, bp,
-                                                                n, out, ctl, nullptr);
-        if (var)
-            return key32 ? bound_and_reduce<R, uint32_t, Item32>(ctx, s, pl, cur, bstart, bcnt, B, bp,
+        if constexpr (sizeof(R) == 16) {
+            return fail(ctx, DPG_ERR_HIP, "internal: R16 outside the pre-aggregate");
+        } else {
+            // MEAN / VARIANCE without SUM (and without per-partition sum
+            // clipping): 24-byte items with the normalised moments only
+            if (var && !(p->metric_mask & DPG_M_SUM) && p->sum_mode != DPG_SUM_CLIP_PARTITION)
+                return key32 ? bound_and_reduce<R, uint32_t, ItemV>(ctx, s, pl, cur, bstart, bcnt, B,
+                                                                    bp, n, out, ctl, nullptr)
+                             : bound_and_reduce<R, uint64_t, ItemV>(ctx, s, pl, cur, bstart, bcnt, B,
+                                                                    bp, n, out, ctl, nullptr);
+            if (var)
+                return key32 ? bound_and_reduce<R, uint32_t, Item32>(ctx, s, pl, cur, bstart, bcnt, B,
+                                                                     bp, n, out, ctl, nullptr)
+                             : bound_and_reduce<R, uint64_t, Item32>(ctx, s, pl, cur, bstart, bcnt, B,
+                                                                     bp, n, out, ctl, nullptr);
+            return key32 ? bound_and_reduce<R, uint32_t, Item16>(ctx, s, pl, cur, bstart, bcnt, B, bp,
                                                                  n, out, ctl, nullptr)
-                         : bound_and_reduce<R, uint64_t, Item32>(ctx, s, pl, cur, bstart, bcnt, B, bp,
+                         : bound_and_reduce<R, uint64_t, Item16>(ctx, s, pl, cur, bstart, bcnt, B, bp,
                                                                  n, out, ctl, nullptr);
-        return key32 ? bound_and_reduce<R, uint32_t, Item16>(ctx, s, pl, cur, bstart, bcnt, B, bp, n,
-                                                             out, ctl, nullptr)
-                     : bound_and_reduce<R, uint64_t, Item16>(ctx, s, pl, cur, bstart, bcnt, B, bp, n,
-                                                             out, ctl, nullptr);
+        }
     };
     r = bound();
     if (r == kRedoLevel2) {
@@ -1301,6 +1306,10 @@ int aggregate_impl(dpg_ctx *ctx, const int64_t *pid, const int64_t *pk, const do
     pl.plb = pl.kbits - bits_total;
     const uint32_t ib = std::max<uint32_t>(1, bits_for((uint64_t)n));
     const bool r8 = (pl.kbits - pl.b1) + pl.pkbits + ib <= 64;
+    // the utility pre-aggregate sums every record's value: R16 records carry
+    // it (DPG_PA_GATHER=1: gather by index as the bounded paths do)
+    if (r8 && pa && value && std::getenv("DPG_PA_GATHER") == nullptr)
+        return pipeline<R16>(ctx, s, pid, pk, value, n, p, out, ctl, pl, pid_min, U, ib, pa);
     if (r8) return pipeline<R8>(ctx, s, pid, pk, value, n, p, out, ctl, pl, pid_min, U, ib, pa);
     return pipeline<R12>(ctx, s, pid, pk, value, n, p, out, ctl, pl, pid_min, U, ib, pa);
 }
