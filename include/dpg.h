@@ -186,16 +186,16 @@ typedef struct dpg_noise_params {
 } dpg_noise_params;
 
 /* One (privacy id, partition) pair of the utility-analysis pre-aggregate
- * (32 bytes): the pair's record count and value sum, the number of
- * partitions its privacy id contributes to and the privacy id's records. */
+ * (24 bytes): the pair's record count and value sum, the number of
+ * partitions its privacy id contributes to and the privacy id's records.
+ * Bit 31 of contributions_leader is the leader flag (dpg_preaggregate sets
+ * it on one pair per privacy id); bits 0-30 are n_contributions. */
 typedef struct dpg_pair_entry {
     uint32_t pk;
     uint32_t count;
     double sum;
     uint32_t n_partitions;
-    uint32_t n_contributions;
-    uint32_t leader;       /* dpg_preaggregate: 1 on one pair per privacy id */
-    uint32_t reserved;
+    uint32_t contributions_leader;  /* n_contributions | leader << 31 */
 } dpg_pair_entry;
 
 /* One row of a MultiParameterConfiguration (analysis/data_structures.py
@@ -310,7 +310,7 @@ int dpg_compact_kept(dpg_ctx *ctx, const uint8_t *keep, const double *out,
  * [partition_start[k], partition_start[k + 1]).  Of *p only n_partitions,
  * public_mask (pairs of other partitions are dropped first), pid_min,
  * pid_count and rec_id_offset are used.  value may be NULL (sums 0).
- * *n_pairs (host) receives the pair count (synchronises the stream); if it
+ * n < 2^31 (else DPG_ERR_UNSUPPORTED).  *n_pairs (host) receives the pair count (synchronises the stream); if it
  * exceeds capacity the call fails with DPG_ERR_INVALID_ARG. */
 int dpg_preaggregate(dpg_ctx *ctx, const int64_t *pid, const int64_t *pk, const double *value,
                      int64_t n, const dpg_bound_params *p, dpg_pair_entry *pairs,
@@ -343,8 +343,8 @@ int dpg_utility_analysis(dpg_ctx *ctx, const dpg_pair_entry *pairs,
 
 /* Dataset histograms over a pre-aggregate sorted by partition key (pairs,
  * partition_start as dpg_preaggregate writes them).  pre_aggregated = 0:
- * the pairs come from dpg_preaggregate, whose `leader` marks one pair per privacy
- * id (the per-privacy-id histograms count those); 1: user-supplied
+ * the pairs come from dpg_preaggregate, whose leader bit marks one pair per
+ * privacy id (the per-privacy-id histograms count those); 1: user-supplied
  * (count, sum, n_partitions, n_contributions) rows, L0 / L1 weighted by
  * 1 / n_partitions per exact value and rounded half to even
  * (computing_histograms.py:81-102, 482-529).  All outputs are device

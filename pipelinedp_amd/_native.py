@@ -70,8 +70,8 @@ class NoiseParams(ctypes.Structure):
 class PairEntry(ctypes.Structure):
     """dpg_pair_entry: one (privacy id, partition) pair of the pre-aggregate."""
     _fields_ = [("pk", ctypes.c_uint32), ("count", ctypes.c_uint32), ("sum", ctypes.c_double),
-                ("n_partitions", ctypes.c_uint32), ("n_contributions", ctypes.c_uint32),
-                ("leader", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+                ("n_partitions", ctypes.c_uint32),
+                ("contributions_leader", ctypes.c_uint32)]  # n_contributions | leader << 31
 
 
 class HistOut(ctypes.Structure):

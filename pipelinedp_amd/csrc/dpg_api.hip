@@ -966,7 +966,10 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     uint32_t F = 1;
     if (n_items > 0) {
         const uint32_t rb = std::max<uint32_t>(1, bits_for((uint64_t)std::max<int64_t>(1, nranges)));
-        const uint32_t b2 = rb > 10 ? std::min<uint32_t>(kMaxBR, rb - 1) : 0u;
+        // two levels split the bits evenly: a sub-tile of 4096-8192 items
+        // writes runs of 16-64 items per digit at both levels (a 4 + 11 split
+        // at config 4's 24 415 ranges wrote runs of ~2 items at level 2)
+        const uint32_t b2 = rb > 10 ? std::min<uint32_t>(kMaxBR, rb / 2) : 0u;
         const uint32_t b1 = rb - b2;
         const uint32_t F1 = nranges <= 1024 ? (uint32_t)std::max<int64_t>(1, nranges) : 1u << b1;
         WS(items2, Item, "items2", n_items);
@@ -1030,7 +1033,8 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
         LAUNCH_CHECK();
         size_t lds_r = (size_t)kRange * 8 * (ItemTraits<Item>::var ? (ItemTraits<Item>::sum ? 3 : 2) : 1) +
                        kRange * 8;
-        k_reduce_items<Item><<<max_tiles, 1024, lds_r, s>>>(sorted, rt, &ctl->ntiles[5], P, po);
+        k_reduce_items<Item><<<max_tiles, 1024, lds_r, s>>>(sorted, rt, &ctl->ntiles[5], rsnt, P,
+                                                         po);
         LAUNCH_CHECK();
     }
     stage(ctx, s, "end");
@@ -1540,7 +1544,8 @@ int dpg_preaggregate(dpg_ctx *ctx, const int64_t *pid, const int64_t *pk, const 
         return fail(ctx, DPG_ERR_INVALID_ARG, "null argument");
     if (p->n_partitions <= 0 || p->n_partitions >= 0xFFFFFFFFll)
         return fail(ctx, DPG_ERR_INVALID_ARG, "n_partitions must be in [1, 2^32-1)");
-    if (n >= 0xFFFFFFFFll) return fail(ctx, DPG_ERR_UNSUPPORTED, "n must be < 2^32 per device");
+    if (n >= 0x7FFFFFFFll)  // n_contributions shares a word with the leader bit
+        return fail(ctx, DPG_ERR_UNSUPPORTED, "n must be < 2^31 per device");
     if (p->pid_count < 0 || p->pid_count > (1ll << 32))
         return fail(ctx, DPG_ERR_INVALID_ARG, "pid_count must be in [0, 2^32]");
     (void)hipSetDevice(ctx->device);

@@ -514,7 +514,7 @@ __global__ __launch_bounds__(kBigThreads) void k_bound_big(
     mark(bp, 6, clk);
     // ---- G: emit kept pairs
     if constexpr (kPA) {
-        // pid leader (pad0 = 1): the pair with the smallest slot of its
+        // pid leader (leader bit set): the pair with the smallest slot of its
         // privacy id (pidslot is dead here: no pid is over a limit)
         for (uint32_t q = tid; q < Cq; q += kBigThreads) pidslot[q] = kNil;
         big_sync();
@@ -551,9 +551,7 @@ __global__ __launch_bounds__(kBigThreads) void k_bound_big(
         if constexpr (kPA) {
             const uint32_t q = (uint32_t)(pkey >> pkb);
             it.npart = pidm[q];
-            it.ncontrib = pidc[q];
-            it.pad0 = pidslot[q] == p ? 1u : 0u;
-            it.pad1 = 0;
+            it.nl = ItemPA::pack_nl(pidc[q], pidslot[q] == p);
         }
         out[atomicAdd(item_cursor, 1u)] = it;
     }

@@ -498,7 +498,7 @@ __device__ __forceinline__ void bound_chunk(const R (&r)[kRPT], uint32_t n, uint
     // ---- G: emit kept pairs (pair-major, dense); clear the tables for the
     // next chunk
     if constexpr (ItemTraits<Item>::preagg) {
-        // pid leader (pad0 = 1): the pair with the smallest slot of its
+        // pid leader (leader bit set): the pair with the smallest slot of its
         // privacy id (pidv is dead here; phase B rewrites it per chunk)
 #pragma unroll
         for (int j = 0; j < kQPT; ++j) {
@@ -536,9 +536,7 @@ __device__ __forceinline__ void bound_chunk(const R (&r)[kRPT], uint32_t n, uint
             const uint32_t q = (uint32_t)(pairtab[p] >> pkb) & (kCq - 1);
             const uint32_t pm = pidm[q];
             it.npart = pm & 0xFFFFu;
-            it.ncontrib = pm >> 16;
-            it.pad0 = pidv[q] == p ? 1u : 0u;
-            it.pad1 = 0;
+            it.nl = ItemPA::pack_nl(pm >> 16, pidv[q] == p);
         }
         items[slot] = it;
     }

@@ -119,13 +119,20 @@ struct alignas(8) ItemV {  // one kept pair with MEAN / VARIANCE moments, no SUM
     double nsq;
 };
 
-struct alignas(16) ItemPA {  // one (pid, pk) pair of the utility-analysis pre-aggregate
+// 24 bytes: the utility sweep streams the pairs three times (two partition
+// levels and the accumulate), so the leader flag rides in the top bit of the
+// privacy id's record count (n < 2^31 per dpg_preaggregate call)
+struct alignas(8) ItemPA {  // one (pid, pk) pair of the utility-analysis pre-aggregate
     uint32_t pk;
-    uint32_t cnt;       // records of the pair
-    double sum;         // sum of their values (unclipped)
-    uint32_t npart;     // partitions the privacy id contributes to
-    uint32_t ncontrib;  // records of the privacy id
-    uint32_t pad0, pad1;
+    uint32_t cnt;    // records of the pair
+    double sum;      // sum of their values (unclipped)
+    uint32_t npart;  // partitions the privacy id contributes to
+    uint32_t nl;     // records of the privacy id | leader << 31
+    __host__ __device__ uint32_t ncontrib() const { return nl & 0x7FFFFFFFu; }
+    __host__ __device__ bool leader() const { return (nl >> 31) != 0; }
+    __host__ __device__ static uint32_t pack_nl(uint32_t nc, bool lead) {
+        return (nc & 0x7FFFFFFFu) | (lead ? 0x80000000u : 0u);
+    }
 };
 
 // ------------------------------------------------------------ privacy-id hash

@@ -13,7 +13,7 @@
 //
 // Input: the pre-aggregate of dpg_preaggregate, sorted by partition key, one
 // entry per pair: (pk, count, sum, n_partitions, n_contributions, leader)
-// where `leader` (pad0) marks one pair per privacy id -- so the per-pid
+// where `leader` (bit 31 of the record count) marks one pair per privacy id -- so the per-pid
 // histograms count every privacy id once without a pass keyed by pid.
 //
 // Integer bins: index v for v < 1000 (width 1), else 1000 + 900 e + (m - 100)
@@ -113,11 +113,11 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_pairs(const ItemPA *pairs
                 if (e.npart > 0) {
                     const double w = 1.0 / (double)e.npart;
                     atomicAdd(&a.w0[e.npart], w);
-                    atomicAdd(&a.w1[e.ncontrib], w);
+                    atomicAdd(&a.w1[e.ncontrib()], w);
                 }
-            } else if (e.pad0) {
+            } else if (e.leader()) {
                 hi_add(small[0], a, 0, e.npart);
-                hi_add(small[1], a, 1, e.ncontrib);
+                hi_add(small[1], a, 1, e.ncontrib());
             }
             lo = fmin(lo, e.sum);
             hi = fmax(hi, e.sum);
@@ -160,7 +160,7 @@ __global__ __launch_bounds__(kHistThreads) void k_pa_max(const ItemPA *pairs, in
     for (int64_t i = (int64_t)blockIdx.x * kHistThreads + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * kHistThreads) {
         a = max(a, pairs[i].npart);
-        b = max(b, pairs[i].ncontrib);
+        b = max(b, pairs[i].ncontrib());
     }
     if (a) atomicMax(&mx[0], a);
     if (b) atomicMax(&mx[1], b);

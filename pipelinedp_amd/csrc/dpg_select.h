@@ -20,11 +20,14 @@ struct Partials {
 };
 
 // combine_accumulators_per_key (pipeline_backend.py:555-565): the kept pairs
-// of one partition-key range are summed in LDS, then added to the dense
-// partials with coalesced global atomics (hot ranges span many tiles).
+// of one partition-key range are summed in LDS, then written to the dense
+// partials: by plain coalesced stores of the whole range when this tile is
+// the range's only one (full-line writes, no read of the zero-filled
+// partials), by coalesced global atomics when a hot range spans several.
 template <class Item>
 __global__ __launch_bounds__(1024) void k_reduce_items(const Item *items, const TileDesc *tiles,
-                                                       const uint32_t *ntiles, int64_t P,
+                                                       const uint32_t *ntiles,
+                                                       const uint32_t *seg_ntiles, int64_t P,
                                                        Partials out) {
     constexpr bool kVar = ItemTraits<Item>::var;
     constexpr bool kSum = ItemTraits<Item>::sum;
@@ -33,11 +36,13 @@ __global__ __launch_bounds__(1024) void k_reduce_items(const Item *items, const 
     double *s_sum = reinterpret_cast<double *>(smem);
     double *s_nsum = s_sum + (kSum ? kRange : 0);
     double *s_nsq = s_nsum + kRange;
-    uint32_t *s_rows = reinterpret_cast<uint32_t *>(smem + kArr * kRange * 8);
-    uint32_t *s_cnt = s_rows + kRange;
+    // rows in the high word, records in the low one: one LDS atomic for both
+    // (a device holds < 2^32 records, so neither word overflows)
+    unsigned long long *s_rc = reinterpret_cast<unsigned long long *>(smem + kArr * kRange * 8);
     const uint32_t t = blockIdx.x;
     if (t >= *ntiles) return;
     const TileDesc td = tiles[t];
+    const bool sole = seg_ntiles[td.seg] == 1;
     const int tid = threadIdx.x;
     for (int k = tid; k < kRange; k += 1024) {
         if (kSum) s_sum[k] = 0.0;
@@ -45,8 +50,7 @@ __global__ __launch_bounds__(1024) void k_reduce_items(const Item *items, const 
             s_nsum[k] = 0.0;
             s_nsq[k] = 0.0;
         }
-        s_rows[k] = 0;
-        s_cnt[k] = 0;
+        s_rc[k] = 0;
     }
     __syncthreads();
     // kRU item loads per thread in flight before their LDS atomics (one
@@ -61,8 +65,7 @@ __global__ __launch_bounds__(1024) void k_reduce_items(const Item *items, const 
         for (int u = 0; u < kRU; ++u) {
             if (i0 + u * 1024 + tid >= td.end) continue;
             const uint32_t k = it[u].pk & (kRange - 1);
-            atomicAdd(&s_rows[k], 1u);
-            atomicAdd(&s_cnt[k], it[u].cnt);
+            atomicAdd(&s_rc[k], (1ull << 32) | (unsigned long long)it[u].cnt);
             if constexpr (kSum)
                 if (it[u].sum != 0.0) atomicAdd(&s_sum[k], it[u].sum);
             if constexpr (kVar) {
@@ -74,10 +77,23 @@ __global__ __launch_bounds__(1024) void k_reduce_items(const Item *items, const 
     __syncthreads();
     const int64_t pk0 = (int64_t)td.seg << kRangeBits;
     for (int k = tid; k < kRange; k += 1024) {
-        int64_t pk = pk0 + k;
-        if (pk >= P || s_rows[k] == 0) continue;
-        atomicAdd((unsigned long long *)&out.rows[pk], (unsigned long long)s_rows[k]);
-        atomicAdd((unsigned long long *)&out.count[pk], (unsigned long long)s_cnt[k]);
+        const int64_t pk = pk0 + k;
+        if (pk >= P) break;
+        const unsigned long long rc = s_rc[k];
+        const int64_t rows = (int64_t)(rc >> 32), cnt = (int64_t)(rc & 0xFFFFFFFFull);
+        if (sole) {
+            out.rows[pk] = rows;
+            out.count[pk] = cnt;
+            if (kSum && out.sum) out.sum[pk] = s_sum[k];
+            if constexpr (kVar) {
+                if (out.nsum) out.nsum[pk] = s_nsum[k];
+                if (out.nsq) out.nsq[pk] = s_nsq[k];
+            }
+            continue;
+        }
+        if (rows == 0) continue;
+        atomicAdd((unsigned long long *)&out.rows[pk], (unsigned long long)rows);
+        atomicAdd((unsigned long long *)&out.count[pk], (unsigned long long)cnt);
         if (kSum && out.sum) atomicAdd(&out.sum[pk], s_sum[k]);
         if constexpr (kVar) {
             if (out.nsum) atomicAdd(&out.nsum[pk], s_nsum[k]);

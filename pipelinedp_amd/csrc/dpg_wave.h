@@ -886,7 +886,7 @@ bool overp[kWQPL];
     {
         if constexpr (ItemTraits<Item>::preagg) {
             // pid leader: the pair with the smallest dense id of its privacy
-            // id carries pad0 = 1, so dataset histograms count every privacy
+            // id carries the leader bit, so dataset histograms count every privacy
             // id once (pidv, the pid hashes, is dead here and is rewritten
             // for the next chunk's occupied slots)
 #pragma unroll
@@ -926,9 +926,7 @@ bool overp[kWQPL];
                     const uint32_t q = (uint32_t)(pkv[j] >> pkb) & (kWCq - 1);
                     const uint32_t pm = pidm[q];
                     it.npart = pm & 0xFFFFu;
-                    it.ncontrib = pm >> 16;
-                    it.pad0 = pidv[q] == lane + 64u * j ? 1u : 0u;
-                    it.pad1 = 0;
+                    it.nl = ItemPA::pack_nl(pm >> 16, pidv[q] == lane + 64u * j);
                 }
                 items[nitems + lanes_below(be)] = it;
             }

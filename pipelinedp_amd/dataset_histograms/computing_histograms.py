@@ -5,7 +5,7 @@ compute_dataset_histograms (:420-474) builds six histograms from the rows:
 L0 / L1 contributions per privacy id, LINF records and LINF_SUM value sum
 per (privacy id, partition) pair, and records / privacy ids per partition.
 The reference runs a dozen backend group-bys over the rows.  Here it is two
-C-ABI calls: dpg_preaggregate (one 32-byte entry per pair, one pair per
+C-ABI calls: dpg_preaggregate (one 24-byte entry per pair, one pair per
 privacy id marked as its leader) and dpg_dataset_histograms (csrc/
 dpg_hist.h: streaming passes over the pairs and the partitions into
 LDS-privatised bins).  The host only turns the few thousand non-empty bins

@@ -1,14 +1,14 @@
 """The per-(privacy id, partition) pre-aggregate on the device.
 
 One entry per distinct (privacy id, partition) pair -- (pk, count, sum,
-n_partitions, n_contributions, leader), 32 bytes (dpg_pair_entry) -- sorted
+n_partitions, n_contributions | leader << 31), 24 bytes (dpg_pair_entry) -- sorted
 by partition key, with partition_start[P + 1] delimiting each partition's
 pairs.  Utility analysis and the dataset histograms both start from it:
 
   raw rows       analysis/pre_aggregation.py:19-61 and
                  analysis/contribution_bounders.py:37-77, computed by
                  dpg_preaggregate (no bounding, values summed unclipped);
-                 `leader` marks one pair per privacy id
+                 the leader bit marks one pair per privacy id
   pre-aggregated PreAggregateExtractors rows (partition key, (count, sum,
                  n_partitions, n_contributions)) as the reference takes them
                  (pipeline_dp/data_extractors.py PreAggregateExtractors),
@@ -25,13 +25,15 @@ from pipelinedp_amd import _native
 from pipelinedp_amd import columnar
 
 PAIR_DTYPE = np.dtype([("pk", "<u4"), ("count", "<u4"), ("sum", "<f8"), ("np", "<u4"),
-                       ("nc", "<u4"), ("leader", "<u4"), ("r", "<u4")])
-assert PAIR_DTYPE.itemsize == ctypes.sizeof(_native.PairEntry) == 32
+                       ("ncl", "<u4")])
+assert PAIR_DTYPE.itemsize == ctypes.sizeof(_native.PairEntry) == 24
+PAIR_WORDS = PAIR_DTYPE.itemsize // 8   # float64 words per pair (device tensors)
+NC_MASK = 0x7FFFFFFF                    # n_contributions bits of "ncl"
 
 
 @dataclasses.dataclass
 class PairSet:
-    pairs: torch.Tensor             # device float64[cap, 4] viewed as dpg_pair_entry
+    pairs: torch.Tensor             # device float64[cap, 3] viewed as dpg_pair_entry
     starts: torch.Tensor            # device int64[P + 1]
     n_partitions: int
     n_pairs: int
@@ -52,7 +54,7 @@ def device_pairs(col, extractors, backend, public_partitions, dev) -> PairSet:
     if enc.public_mask is not None:
         bound.public_mask = enc.public_mask.data_ptr()
     cap = max(enc.n, 1)
-    pairs = torch.empty((cap, 4), dtype=torch.float64, device=dev)
+    pairs = torch.empty((cap, PAIR_WORDS), dtype=torch.float64, device=dev)
     starts = torch.empty(P + 1, dtype=torch.int64, device=dev)
     with torch.cuda.device(dev):
         sptr = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
@@ -92,9 +94,10 @@ def host_preaggregated_pairs(col, extractors, public_partitions, dev) -> PairSet
         arr["sum"][:n] = pre_a[:, 1]
         arr["np"][:n] = pre_a[:, 2]
         if pre_a.shape[1] > 3:
-            arr["nc"][:n] = pre_a[:, 3]
+            # the word's top bit is the leader flag (unused for these rows)
+            arr["ncl"][:n] = np.minimum(pre_a[:, 3], NC_MASK)
     starts = np.searchsorted(ids[order], np.arange(P + 1)).astype(np.int64)
-    pairs = torch.from_numpy(arr.view(np.float64).reshape(-1, 4).copy()).to(dev)
+    pairs = torch.from_numpy(arr.view(np.float64).reshape(-1, PAIR_WORDS).copy()).to(dev)
     return PairSet(pairs, torch.from_numpy(starts).to(dev), P, n, table, pub_mask)
 
 

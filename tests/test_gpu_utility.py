@@ -182,3 +182,47 @@ def test_64_config_sweep_matches_oracle(built, public):
         uc.assert_close(want, per[key], f"per{key}", atol=1e-7, rtol=1e-7)
     for want, got in zip(want_rep, reports):
         uc.assert_close(want, got, "report", atol=1e-7, rtol=1e-7)
+
+
+def _sorted_pairs(ps):
+    from pipelinedp_amd import pre_aggregation as pa
+    a = pa.to_numpy(ps)
+    nc = a["ncl"] & pa.NC_MASK
+    return a[np.lexsort((nc, a["np"], a["sum"], a["count"], a["pk"]))], ps.starts.cpu()
+
+
+@pytest.mark.parametrize("exact", [True, False], ids=["quarter_values", "uniform_values"])
+def test_preaggregate_value_records_match_gather_path(built, exact, monkeypatch):
+    """dpg_preaggregate carries the value inside 16-byte records through the
+    partition levels (R16); DPG_PA_GATHER=1 keeps 8-byte records and gathers
+    each value by record index.  Both must produce the same pairs: counts,
+    partition / contribution counts bit-exact, one leader pair per privacy id
+    in each (which pair leads follows the record order, so it may differ),
+    sums exact for quarter-integer values (any summation order) and within
+    1e-12 relative otherwise."""
+    from pipelinedp_amd import pre_aggregation as pa
+    rng = np.random.default_rng(77 + exact)
+    n, n_pid, P = 1_500_000, 30_000, 5_000
+    pid = rng.integers(0, n_pid, n)
+    w = np.arange(1, P + 1, dtype=np.float64) ** -1.05
+    pk = rng.choice(P, size=n, p=w / w.sum())
+    val = rng.integers(-8, 40, n) * 0.25 if exact else rng.uniform(-1, 6, n)
+    cols = pdp.ColumnarData(pid=torch.as_tensor(pid), pk=torch.as_tensor(pk),
+                            value=torch.as_tensor(val), n_partitions=P)
+    ex = pdp.DataExtractors("pid", "pk", "value")
+    be = pdp.MI355XBackend(device=0, seed=5)
+    dev = torch.device("cuda", 0)
+    monkeypatch.delenv("DPG_PA_GATHER", raising=False)
+    got, gs = _sorted_pairs(pa.device_pairs(cols, ex, be, None, dev))
+    monkeypatch.setenv("DPG_PA_GATHER", "1")
+    want, ws = _sorted_pairs(pa.device_pairs(cols, ex, be, None, dev))
+    assert torch.equal(gs, ws)
+    assert len(got) == len(want) == len(np.unique(pid * P + pk))
+    for f in ("pk", "count", "np"):
+        np.testing.assert_array_equal(got[f], want[f], err_msg=f)
+    np.testing.assert_array_equal(got["ncl"] & pa.NC_MASK, want["ncl"] & pa.NC_MASK)
+    assert int((got["ncl"] >> 31).sum()) == int((want["ncl"] >> 31).sum()) == len(np.unique(pid))
+    if exact:
+        np.testing.assert_array_equal(got["sum"], want["sum"])
+    else:
+        np.testing.assert_allclose(got["sum"], want["sum"], rtol=1e-12, atol=1e-9)
