@@ -242,8 +242,8 @@ def stage_design_bytes(stage: str, n: int, rec: int, item: int, kept_recs: int,
         return 8 * n
     if stage == "partition1:hist":
         return 8 * n                      # pid column
-    if stage == "partition1:scatter":
-        return (16 + rec) * n             # pid + pk in, packed record out
+    if stage in ("partition1:scatter", "partition1:pieces"):
+        return (16 + rec) * n             # pid + pk in, packed record out (pieces: no hist pass)
     if stage in ("partition2:hist", "refine:hist"):
         return rec * n
     if stage in ("partition2:scatter", "refine:scatter", "partition2:team"):

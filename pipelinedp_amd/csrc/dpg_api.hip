@@ -50,6 +50,9 @@ constexpr uint32_t kChunkGroup = 32;     // fine buckets per packing thread
 // Status of bound_and_reduce when a team level-2 barrier timed out (err bit
 // 8): the caller redoes level 2 with the histogram path.
 constexpr int kRedoLevel2 = -100;
+#ifndef DPG_IPT_PC
+#define DPG_IPT_PC 10  // records per thread of the histogram-free level 1
+#endif
 
 struct Buf {
     void *p = nullptr;
@@ -367,7 +370,7 @@ int run_level_grouped(dpg_ctx *ctx, hipStream_t s, const Src &src, uint32_t S,
     stage(ctx, s, (t + ":scatter").c_str());
     const uint32_t gs = std::min<uint32_t>(max_subs, (uint32_t)ctx->n_cu);  // one per CU
     kern<<<gs, kScatThreads, lds, s>>>(src, tiles, ntiles_dev, F, bits, nullptr, base, out, xq,
-                                       nullptr, nullptr, nullptr, 1u, hist);
+                                       nullptr, nullptr, nullptr, 1u, hist, 0u, 0u, nullptr);
     LAUNCH_CHECK();
     *base_out = base;
     *tot_out = tot;
@@ -458,7 +461,8 @@ int run_level(dpg_ctx *ctx, hipStream_t s, const Src &src, uint32_t S, const int
                                    : max_tiles;
     if (xcd_local) gs = std::min<uint32_t>(max_tiles, (uint32_t)ctx->n_cu);  // one per CU
     kern<<<gs, kScatThreads, lds, s>>>(src, tiles, ntiles_dev, F, bits, hist, base, out, xq,
-                                       C > 1 ? ctot : nullptr, stb, snt, C, nullptr);
+                                       C > 1 ? ctot : nullptr, stb, snt, C, nullptr, 0u, 0u,
+                                       nullptr);
     LAUNCH_CHECK();
     *base_out = base;
     *tot_out = tot;
@@ -1041,12 +1045,116 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     return DPG_OK;
 }
 
+// Histogram-free level 1 (k_scatter's piece mode): region (x, d) of C
+// records starts at (8 d + x) C, so a bucket's 8 pieces are neighbours.
+__global__ void k_region_base(int64_t *rbase, uint32_t F, uint32_t C) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= 8 * F) return;
+    const uint32_t x = i / F, d = i % F;
+    rbase[i] = ((int64_t)d * 8 + x) * C;
+}
+
+// Bucket totals of the pieces and the buckets' starts in the compact level-2
+// output (one workgroup; F <= 2048).
+__global__ __launch_bounds__(1024) void k_piece_totals(const uint32_t *cum, uint32_t F,
+                                                       uint32_t *tot, uint32_t *ptot,
+                                                       int64_t *ostart) {
+    __shared__ uint32_t sh[16];
+    const uint32_t d0 = 2 * threadIdx.x;
+    uint32_t c[2], x = 0;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        c[u] = 0;
+        uint32_t cp = 0;  // padded: each piece rounded up to even (team pair loads)
+        if (d0 + u < F)
+            for (int r = 0; r < 8; ++r) {
+                const uint32_t y = cum[(size_t)r * F + d0 + u];
+                c[u] += y;
+                cp += (y + 1u) & ~1u;
+            }
+        if (d0 + u < F) ptot[d0 + u] = cp;
+        x += c[u];
+    }
+    uint32_t total;
+    uint32_t e = block_excl_scan_1024(x, sh, total);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        if (d0 + u < F) {
+            tot[d0 + u] = c[u];
+            ostart[d0 + u] = e;
+        }
+        e += c[u];
+    }
+}
+
+// Capacity C of one region, or 0 when the piece layout does not apply (the
+// record positions of all 8 F regions plus the dump area must stay below
+// 2^32).  Hashed privacy ids spread a level-1 digit's records evenly over
+// the XCDs' static tile shares; 25 % + 4096 records of slack, an overflow
+// redoes the level with the histogram path (DPG_DEBUG_PIECE_CAP: a test
+// hook forcing a smaller capacity).
+uint32_t piece_capacity(int64_t n, uint32_t F, int64_t sub) {
+    double c = 1.25 * (double)n / (8.0 * F) + 4096.0;
+    if (const char *e = std::getenv("DPG_DEBUG_PIECE_CAP")) c = std::max(2.0, std::atof(e));
+    const double slots = c * 8.0 * F + (double)sub;
+    if (slots >= 4294967295.0) return 0;
+    return (uint32_t)c & ~1u;  // even: the team reads pieces by 16-byte pairs
+}
+
+template <class R, int IPT>
+int run_level1_pieces(dpg_ctx *ctx, hipStream_t s, const SrcSoAKey<R, true> &src, int64_t n,
+                      uint32_t F, uint32_t bits, uint32_t C, R *out, Control *ctl,
+                      PieceTab *pt, uint32_t *host_tot) {
+    int st = DPG_OK;
+    const int64_t sub = (int64_t)kScatThreads * IPT;
+    const uint32_t nt = (uint32_t)((n + sub - 1) / sub);
+    WS(tiles, TileDesc, "pieces.tiles", nt);
+    WS(stb, uint32_t, "pieces.stb", 1);
+    WS(snt, uint32_t, "pieces.snt", 1);
+    WS(rbase, int64_t, "pieces.rbase", (size_t)8 * F);
+    WS(cum, uint32_t, "pieces.cum", (size_t)8 * F);
+    WS(tot, uint32_t, "pieces.tot", F);
+    WS(ptot, uint32_t, "pieces.ptot", F);
+    WS(ostart, int64_t, "pieces.ostart", F);
+    HIP_TRY(hipMemsetAsync(cum, 0, (size_t)8 * F * 4, s));
+    HIP_TRY(hipMemsetAsync(&ctl->ntiles[0], 0, 4, s));
+    stage(ctx, s, "partition1:pieces");
+    k_region_base<<<(8 * F + 255) / 256, 256, 0, s>>>(rbase, F, C);
+    LAUNCH_CHECK();
+    k_build_tiles_single<<<(nt + 255) / 256, 256, 0, s>>>(n, sub, 1u, tiles, stb, snt,
+                                                         &ctl->ntiles[0], XcdQueues{});
+    LAUNCH_CHECK();
+    using Src = SrcSoAKey<R, true>;
+    constexpr size_t lds = scatter_lds<Src, R, IPT, 2048>();
+    static_assert(lds <= 160 * 1024, "scatter LDS");
+    auto kern = k_scatter<Src, R, IPT, 2048, false>;
+    if (bits <= (uint32_t)agg_bits()) return fail(ctx, DPG_ERR_HIP, "internal: piece level fan-out");
+    (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    const uint32_t gs = std::min<uint32_t>(nt, (uint32_t)ctx->n_cu);  // one per CU
+    kern<<<gs, kScatThreads, lds, s>>>(src, tiles, &ctl->ntiles[0], F, bits, nullptr, rbase, out,
+                                       XcdQueues{}, nullptr, nullptr, nullptr, 1u, cum, C,
+                                       (uint32_t)((uint64_t)8 * F * C), &ctl->err);
+    LAUNCH_CHECK();
+    k_piece_totals<<<1, 1024, 0, s>>>(cum, F, tot, ptot, ostart);
+    LAUNCH_CHECK();
+    // totals and the error word reach the host for the overflow / team checks
+    if (!ctx->tot_ev && hipEventCreateWithFlags(&ctx->tot_ev, hipEventDisableTiming) != hipSuccess)
+        return fail(ctx, DPG_ERR_HIP, "hipEventCreate (totals)");
+    HIP_TRY(hipMemcpyAsync(host_tot, tot, (size_t)F * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(host_tot + 4095, &ctl->err, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipEventRecord(ctx->tot_ev, s));
+    *pt = PieceTab{rbase, cum, tot, ptot, ostart, F};
+    return DPG_OK;
+}
+
 // Level 2 by teams of workgroups (dpg_team.h): S level-1 buckets, each
-// <= (n_cu / 8) * kTeamSub records (the caller checked the level-1 totals).
+// <= (n_cu / 8) * kTeamSub records (the caller checked the level-1 totals);
+// pt: the buckets are the pieces of the histogram-free level 1.
 template <class R>
 int run_team_level2(dpg_ctx *ctx, hipStream_t s, const SrcAoS<R> &src, uint32_t S, uint32_t F2,
                     const int64_t *seg_start, const uint32_t *seg_cnt, R *out, Control *ctl,
-                    int64_t **base_out, uint32_t **tot_out) {
+                    int64_t **base_out, uint32_t **tot_out, const PieceTab *pt = nullptr) {
     int st = DPG_OK;
     const uint32_t F = kTeamF;
     const size_t words = (size_t)8 * 3 * F + 8 * kTeamArriveStride + 32;
@@ -1064,11 +1172,15 @@ int run_team_level2(dpg_ctx *ctx, hipStream_t s, const SrcAoS<R> &src, uint32_t 
         k_set_bits<<<1, 1, 0, s>>>(&ctl->err, 8u);
         LAUNCH_CHECK();
     }
-    const void *k = (const void *)k_part2_team<R>;
+    const void *k = pt ? (const void *)k_part2_team<R, true> : (const void *)k_part2_team<R, false>;
     (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)team_lds<R>());
     stage(ctx, s, "partition2:team");
-    k_part2_team<R><<<(unsigned)ctx->n_cu, kScatThreads, team_lds<R>(), s>>>(
-        src, seg_start, seg_cnt, S, F2, out, base, tot, ts);
+    if (pt)
+        k_part2_team<R, true><<<(unsigned)ctx->n_cu, kScatThreads, team_lds<R>(), s>>>(
+            src, seg_start, seg_cnt, S, F2, out, base, tot, ts, *pt);
+    else
+        k_part2_team<R, false><<<(unsigned)ctx->n_cu, kScatThreads, team_lds<R>(), s>>>(
+            src, seg_start, seg_cnt, S, F2, out, base, tot, ts, PieceTab{});
     LAUNCH_CHECK();
     *base_out = base;
     *tot_out = tot;
@@ -1081,8 +1193,6 @@ int pipeline(dpg_ctx *ctx, hipStream_t s, const int64_t *pid, const int64_t *pk,
              Control *ctl, const Plan &pl, int64_t pid_min, uint64_t U, uint32_t ib, PaOut *pa) {
     int st = DPG_OK;
     const bool var = (p->metric_mask & (DPG_M_MEAN | DPG_M_VARIANCE)) != 0;
-    WS(recA, R, "recA", n);
-    WS(recB, R, "recB", n);
     const Fmt f{ib, pl.pkbits, pl.kbits, pl.b1};
     const HashK H = make_hash(pl.kbits);
     // ---- level 1: SoA -> records bucketed by the top b1 hash bits
@@ -1145,20 +1255,70 @@ int pipeline(dpg_ctx *ctx, hipStream_t s, const int64_t *pid, const int64_t *pk,
         ctx->pin_tot = nullptr;
         team = false;
     }
-    int r = run_level<SrcSoAKey<R>, R, Ipt<R>::L1, 2048>(ctx, s, s1, 1u, nullptr, nullptr,
-                                                         &ctl->n_scalar, n, F1, pl.b1, recA,
-                                                         "partition1", &bstart, &bcnt, &ctl->ntiles[0],
-                                                         nullptr, l1_xcd, l1_subs, l1_grp,
-                                                         team ? ctx->pin_tot : nullptr);
-    if (r) return r;
-    if (team) {
-        HIP_TRY(hipEventSynchronize(ctx->tot_ev));
-        uint32_t mx = 0;
-        for (uint32_t d = 0; d < F1; ++d) mx = std::max(mx, ctx->pin_tot[d]);
-        team = (uint64_t)mx <= (uint64_t)team_T * kTeamSub;
+    // level 1 without a histogram pass (k_scatter's piece mode, dpg_team.h
+    // PieceTab): 8-byte records whose level 2 runs by teams; every XCD
+    // appends to fixed-capacity regions, so recA holds 8 F1 regions of
+    // `pcap` records (+ a dump area).  Opt-in (DPG_L1_PIECES=1): same-box
+    // A/B at config 2, level 1 8.8 -> 7.4 ms but the team level 2 reading
+    // the pieces 5.1 -> 6.8 ms, a net loss.
+    constexpr int kIptPc = DPG_IPT_PC;
+    const int64_t subPc = (int64_t)kScatThreads * kIptPc;
+    uint32_t pcap = 0;
+    bool pieces = false;
+    if constexpr (sizeof(R) == 8) {
+        if (team && env_int("DPG_L1_PIECES", 0) != 0 && n >= ((int64_t)1 << 22) &&
+            pl.b1 > (uint32_t)agg_bits()) {
+            pcap = piece_capacity(n, F1, subPc);
+            pieces = pcap > 0;
+        }
     }
-    const int64_t *bstart1 = bstart;
-    const uint32_t *bcnt1 = bcnt;
+    // (the histogram path may redo level 1 into the same buffer: >= n)
+    WS(recA, R, "recA", pieces ? std::max<int64_t>(n, (int64_t)8 * F1 * pcap + subPc) : n);
+    WS(recB, R, "recB", n);
+    int64_t *bstart1 = nullptr;
+    uint32_t *bcnt1 = nullptr;
+    auto level1_std = [&](bool with_tot) -> int {
+        return run_level<SrcSoAKey<R>, R, Ipt<R>::L1, 2048>(
+            ctx, s, s1, 1u, nullptr, nullptr, &ctl->n_scalar, n, F1, pl.b1, recA, "partition1",
+            &bstart1, &bcnt1, &ctl->ntiles[0], nullptr, l1_xcd, l1_subs, l1_grp,
+            with_tot ? ctx->pin_tot : nullptr);
+    };
+    PieceTab ptab{};
+    int r = DPG_OK;
+    if constexpr (sizeof(R) == 8) {
+        if (pieces) {
+            SrcSoAKey<R, true> sp{pid, pk, p->public_mask, pl.P, pid_min, U, H, f,
+                                  low_mask(pl.kbits - pl.b1 + pl.pkbits), pl.kbits - pl.b1,
+                                  &ctl->err};
+            r = run_level1_pieces<R, kIptPc>(ctx, s, sp, n, F1, pl.b1, pcap, recA, ctl, &ptab,
+                                             ctx->pin_tot);
+            if (r) return r;
+            HIP_TRY(hipEventSynchronize(ctx->tot_ev));
+            uint32_t mx = 0;
+            for (uint32_t d = 0; d < F1; ++d) mx = std::max(mx, ctx->pin_tot[d]);
+            const bool over = (ctx->pin_tot[4095] & 16u) != 0;
+            // a member's share is its 1/T of the padded bucket (<= 8 slots of
+            // padding) rounded up to even: within kTeamSub records
+            if (over || (uint64_t)mx + 8 > (uint64_t)team_T * (kTeamSub - 2)) {
+                std::fprintf(stderr, "[dpg] histogram-free level 1: %s; redone with the histogram path\n",
+                             over ? "a region overflowed" : "a bucket exceeds the team capacity");
+                HIP_TRY(hipMemsetAsync(&ctl->err, 0, 4, s));
+                pieces = false;
+            }
+        }
+    }
+    if (!pieces) {
+        r = level1_std(team);
+        if (r) return r;
+        if (team) {
+            HIP_TRY(hipEventSynchronize(ctx->tot_ev));
+            uint32_t mx = 0;
+            for (uint32_t d = 0; d < F1; ++d) mx = std::max(mx, ctx->pin_tot[d]);
+            team = (uint64_t)mx <= (uint64_t)team_T * kTeamSub;
+        }
+    }
+    bstart = bstart1;
+    bcnt = bcnt1;
     const R *cur = recA;
     uint32_t B = F1;
     auto level2_grouped = [&]() -> int {
@@ -1190,7 +1350,8 @@ int pipeline(dpg_ctx *ctx, hipStream_t s, const int64_t *pid, const int64_t *pk,
         if constexpr (sizeof(R) == 8) {
             if (team) {
                 SrcAoS<R> s2{recA, f, shift2, F2 - 1};
-                r = run_team_level2<R>(ctx, s, s2, F1, F2, bstart1, bcnt1, recB, ctl, &bstart, &bcnt);
+                r = run_team_level2<R>(ctx, s, s2, F1, F2, bstart1, bcnt1, recB, ctl, &bstart, &bcnt,
+                                       pieces ? &ptab : nullptr);
             }
         }
         if (!team) {
@@ -1242,6 +1403,12 @@ int pipeline(dpg_ctx *ctx, hipStream_t s, const int64_t *pid, const int64_t *pk,
         HIP_TRY(hipMemsetAsync(&ctl->err, 0, 4, s));
         HIP_TRY(hipMemsetAsync(&ctl->n_chunks, 0,
                                offsetof(Control, pid_lo) - offsetof(Control, n_chunks), s));
+        if (pieces) {
+            // the grouped level 2 reads a contiguous level 1
+            r = level1_std(false);
+            if (r) return r;
+            pieces = false;
+        }
         r = level2_grouped();
         if (r) return r;
         r = bound();

@@ -86,6 +86,18 @@ struct RecOps<R12> {
     }
 };
 
+// One value gathered by record index (the sort kernels' gathers).
+template <class I>
+__device__ __forceinline__ double gather_value(const double *value, I idx) {
+#if DPG_EXP_NO_GATHER  // experiment: what the gathers cost (values read as 0)
+    (void)value;
+    (void)idx;
+    return 0.0;
+#else
+    return value[idx];
+#endif
+}
+
 // The value of a record: carried in an R16, else gathered from the input
 // column by the record's index.
 template <class R>

@@ -61,6 +61,16 @@ struct HasTilePrefetch<Src, decltype((void)Src::kTilePrefetch)> {
     static constexpr bool value = Src::kTilePrefetch && DPG_XTILE_PF;
 };
 
+// Piece-mode sources (k_scatter without a histogram pass, see there).
+template <class Src, class = void>
+struct HasPieces {
+    static constexpr bool value = false;
+};
+template <class Src>
+struct HasPieces<Src, decltype((void)Src::kPieces)> {
+    static constexpr bool value = Src::kPieces;
+};
+
 // Sources without a pair view (kPairs false) take the one-record loop.
 template <class Src, class = void>
 struct HasPairs {
@@ -99,22 +109,27 @@ __device__ __forceinline__ TileDesc uniform_tile(const TileDesc *tiles, uint32_t
 // Drops records of non-public partitions.  Keys outside the declared ranges
 // raise err bit 1 (the call then fails before any bucket is bounded); such a
 // record is still kept so that the scatter agrees with the histogram.
-template <class R>
+//
+// kFull (the histogram-free level 1, k_scatter's piece mode): the scatter
+// loads the whole privacy id and raises the range error itself.
+template <class R, bool kFull = false>
 struct SrcSoAKey {
     static constexpr bool kDigitFromRec = false;
     static constexpr bool kTilePrefetch = true;
+    static constexpr bool kPieces = kFull;
     // the scatter loads only the low word of the privacy id: the digit and
     // the stored key depend on (pid - pid_min) mod 2^32 alone, and the
     // histogram pass, which reads the whole column, raises the range error
     // (12 fewer VGPRs per thread in flight: the level-1 scatter spilled)
     // R16 records carry the value column too (the utility pre-aggregate)
     static constexpr bool kV = sizeof(R) == 16;
+    using PidW = std::conditional_t<kFull, uint64_t, uint32_t>;
     struct RawK {
-        uint32_t pid;
+        PidW pid;
         int64_t pk;
     };
     struct RawV {
-        uint32_t pid;
+        PidW pid;
         int64_t pk;
         double v;
     };
@@ -137,20 +152,31 @@ struct SrcSoAKey {
 #if DPG_L1_NT
     // the key columns are read once: non-temporal loads leave L2 to the
     // scattered runs being written
+    __device__ __forceinline__ PidW fetch_pid(int64_t i) const {
+        if constexpr (kFull)
+            return (uint64_t)__builtin_nontemporal_load(pid + i);
+        else
+            return __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(pid) + 2 * i);
+    }
     __device__ __forceinline__ Raw fetch(int64_t i) const {
         if constexpr (kV)
-            return Raw{__builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(pid) + 2 * i),
-                       __builtin_nontemporal_load(pk + i), __builtin_nontemporal_load(value + i)};
+            return Raw{fetch_pid(i), __builtin_nontemporal_load(pk + i),
+                       __builtin_nontemporal_load(value + i)};
         else
-            return Raw{__builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(pid) + 2 * i),
-                       __builtin_nontemporal_load(pk + i)};
+            return Raw{fetch_pid(i), __builtin_nontemporal_load(pk + i)};
     }
 #else
+    __device__ __forceinline__ PidW fetch_pid(int64_t i) const {
+        if constexpr (kFull)
+            return (uint64_t)pid[i];
+        else
+            return reinterpret_cast<const uint32_t *>(pid)[2 * i];
+    }
     __device__ __forceinline__ Raw fetch(int64_t i) const {
         if constexpr (kV)
-            return Raw{reinterpret_cast<const uint32_t *>(pid)[2 * i], pk[i], value[i]};
+            return Raw{fetch_pid(i), pk[i], value[i]};
         else
-            return Raw{reinterpret_cast<const uint32_t *>(pid)[2 * i], pk[i]};
+            return Raw{fetch_pid(i), pk[i]};
     }
 #endif
     // keep decision shared by the histogram and the scatter (they must agree
@@ -161,8 +187,15 @@ struct SrcSoAKey {
         return !(in_range && !((pub[b >> 3] >> (b & 7)) & 1));
     }
     __device__ __forceinline__ bool decode(const Raw &x, int64_t i, R &r, uint32_t &d) const {
-        const uint32_t a = x.pid - (uint32_t)pid_min;
-        if ((uint64_t)x.pk >= (uint64_t)P) atomicOr(err, 1u);
+        uint32_t a;
+        if constexpr (kFull) {
+            const uint64_t a64 = x.pid - (uint64_t)pid_min;
+            if (a64 >= U || (uint64_t)x.pk >= (uint64_t)P) atomicOr(err, 1u);
+            a = (uint32_t)a64;
+        } else {
+            a = x.pid - (uint32_t)pid_min;
+            if ((uint64_t)x.pk >= (uint64_t)P) atomicOr(err, 1u);
+        }
         const uint32_t h = hk(a, H);
         d = h >> dshift;
         const uint64_t key = (((uint64_t)h << f.pkbits) | (uint64_t)x.pk) & kmask;
@@ -616,11 +649,16 @@ __device__ __forceinline__ uint32_t block_scan_digits_t(const uint32_t *cnt, uin
 // (goff: the group's digit offsets): the sub-tile reserves its run of every
 // digit it holds inside its group by one atomic add, cur[d] += reserved
 // start + cnt[d].  Two barriers: the wave totals' buffer is next written one
-// sub-tile later, behind the caller's own barriers.
-template <int T, int DPT>
+// sub-tile later, behind the caller's own barriers.  Piece mode (kCap): goff
+// are the cursors of fixed-capacity regions; a run that does not fit raises
+// err bit 16 and goes to the dump area at `dump` instead (the host redoes
+// the level with the histogram path).
+template <int T, int DPT, bool kCap = false>
 __device__ __forceinline__ uint32_t scatter_scan_update(uint32_t *cnt, uint32_t *dstart,
                                                         uint32_t *cur, uint32_t F,
-                                                        uint32_t *sh16, uint32_t *goff = nullptr) {
+                                                        uint32_t *sh16, uint32_t *goff = nullptr,
+                                                        uint32_t cap = 0, uint32_t dump = 0,
+                                                        uint32_t *err = nullptr) {
     constexpr int NW = T / 64;
     const uint32_t d0 = DPT * threadIdx.x;
     uint32_t c[DPT], x = 0;
@@ -645,7 +683,17 @@ __device__ __forceinline__ uint32_t scatter_scan_update(uint32_t *cnt, uint32_t 
     for (int u = 0; u < DPT; ++u) {
         if (d0 + u < F) {
             dstart[d0 + u] = e;
-            if (goff) {
+            if constexpr (kCap) {
+                if (c[u]) {
+                    const uint32_t o = atomicAdd(&goff[d0 + u], c[u]);
+                    if (o + c[u] <= cap) {
+                        cur[d0 + u] += o + c[u];
+                    } else {
+                        cur[d0 + u] = dump + e + c[u];
+                        atomicOr(err, 16u);
+                    }
+                }
+            } else if (goff) {
                 if (c[u]) cur[d0 + u] += atomicAdd(&goff[d0 + u], c[u]) + c[u];
             } else {
                 cur[d0 + u] += c[u];
@@ -752,8 +800,15 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
                                                           const uint32_t *cbase = nullptr,
                                                           const uint32_t *seg_tile_base = nullptr,
                                                           const uint32_t *seg_ntiles = nullptr,
-                                                          uint32_t C = 1, uint32_t *goff = nullptr) {
+                                                          uint32_t C = 1, uint32_t *goff = nullptr,
+                                                          uint32_t pcap = 0, uint32_t pdump = 0,
+                                                          uint32_t *perr = nullptr) {
     constexpr int SUB = kScatThreads * IPT;
+    // piece mode (histogram-free level 1): one-sub-tile tiles on a static
+    // schedule; workgroup b appends its runs of digit d to region (b % 8, d)
+    // -- base[(b % 8) F + d], cursor goff[(b % 8) F + d], pcap records -- so
+    // the runs of one XCD's workgroups are adjacent and merge in its L2
+    constexpr bool kPc = HasPieces<Src>::value;
     constexpr bool kSD = !Src::kDigitFromRec;
     constexpr bool kP = HasFetchPairs<Src>::value && IPT % 2 == 0;
     using W = Words<Rec>;
@@ -845,9 +900,11 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
     }
     // grouped mode: the work item is one sub-tile of group td.pad, whose runs
     // are reserved at the digit scan
-    uint32_t *gof = goff ? goff + (size_t)td.pad * F : nullptr;
+    const uint32_t gsel = kPc ? (blockIdx.x & 7u) : td.pad;
+    const uint32_t bsel = kPc ? (blockIdx.x & 7u) : td.seg;
+    uint32_t *gof = goff ? goff + (size_t)gsel * F : nullptr;
     for (uint32_t d = tid; d < F; d += kScatThreads) {
-        cur[d] = (uint32_t)(base[(size_t)td.seg * F + d] +
+        cur[d] = (uint32_t)(base[(size_t)bsel * F + d] +
                             (goff ? 0u : off[(size_t)t * F + d] + (cb ? cb[d] : 0u)));
         cnt[d] = 0;
     }
@@ -890,8 +947,8 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
         }
         if (xq.q && tid == 0 && sb == td.begin) sh_next = nq;
         __syncthreads();
-        const uint32_t total =
-            scatter_scan_update<kScatThreads, FMAX / kScatThreads>(cnt, dstart, cur, F, sh16, gof);
+        const uint32_t total = scatter_scan_update<kScatThreads, FMAX / kScatThreads, kPc>(
+            cnt, dstart, cur, F, sh16, gof, pcap, pdump, perr);
         {
             uint32_t ds[IPT];
 #pragma unroll
@@ -911,7 +968,14 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
             // XCD-local tile, the next tile's first (one load site)
             int64_t lb = nb;
             uint32_t ll = nlim;
-            if constexpr (HasTilePrefetch<Src>::value) {
+            if constexpr (HasTilePrefetch<Src>::value && kPc) {
+                if (nlim == 0 && it + gridDim.x < nt) {
+                    tn = it + gridDim.x;
+                    tdn = uniform_tile(tiles, tn);
+                    lb = tdn.begin;
+                    ll = (uint32_t)min<int64_t>(SUB, tdn.end - tdn.begin);
+                }
+            } else if constexpr (HasTilePrefetch<Src>::value) {
                 if (nlim == 0 && xq.q) {
                     const uint32_t w = __builtin_amdgcn_readfirstlane(sh_next);
                     if (w < xq_len) {
@@ -963,6 +1027,8 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
         tn = __builtin_amdgcn_readfirstlane(xq.q[(size_t)xq_id * xq.stride + w]);
         tdn = uniform_tile(tiles, tn);
         load_sub(tdn.begin, (uint32_t)min<int64_t>(SUB, tdn.end - tdn.begin));
+    } else if (kPc && HasTilePrefetch<Src>::value) {
+        it += gridDim.x;  // tn / tdn set and loaded by the prefetch
     } else if (!xq.q) {
         it += gridDim.x;
         if (it >= nt) break;

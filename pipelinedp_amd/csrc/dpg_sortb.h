@@ -482,7 +482,7 @@ __device__ __forceinline__ int sort_chunk(uint32_t nc, char *smem, const BoundPa
         // records of kept pairs within mcpp gather now; those of over-full
         // pairs only once the sample below has kept them (DPG_SORT_LATE 0:
         // every record of a kept pair gathers here)
-        v[j] = (need_v && kp && (!kSortLate || !ov)) ? bp.value[idx[j]] : 0.0;
+        v[j] = (need_v && kp && (!kSortLate || !ov)) ? gather_value(bp.value, idx[j]) : 0.0;
     }
     uint32_t keepm = kpm;
     maxlen = __builtin_amdgcn_readfirstlane(wave_max_u32(maxlen));
@@ -515,7 +515,7 @@ __device__ __forceinline__ int sort_chunk(uint32_t nc, char *smem, const BoundPa
             if (need_v) {
 #pragma unroll
                 for (int j = 0; j < E; ++j)
-                    if ((overm & keepm) >> j & 1u) v[j] = bp.value[idx[j]];
+                    if ((overm & keepm) >> j & 1u) v[j] = gather_value(bp.value, idx[j]);
             }
         }
     }

@@ -350,7 +350,7 @@ __device__ __forceinline__ int mw_sort_chunk(uint32_t nc, char *smem, const Boun
         const bool ov = sample && kp && len[j] > bp.mcpp;
         overm |= ov ? 1u << j : 0u;
         maxlen = max(maxlen, ov ? len[j] : 0u);
-        v[j] = (need_v && kp && (!kSortLate || !ov)) ? bp.value[idx[j]] : 0.0;  // see dpg_sortb.h
+        v[j] = (need_v && kp && (!kSortLate || !ov)) ? gather_value(bp.value, idx[j]) : 0.0;  // see dpg_sortb.h
     }
     uint32_t keepm = kpm;
     maxlen = __builtin_amdgcn_readfirstlane(mw_max<NW>(maxlen, scr));
@@ -383,7 +383,7 @@ __device__ __forceinline__ int mw_sort_chunk(uint32_t nc, char *smem, const Boun
             if (need_v) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
-                    if ((overm & keepm) >> j & 1u) v[j] = bp.value[idx[j]];
+                    if ((overm & keepm) >> j & 1u) v[j] = gather_value(bp.value, idx[j]);
             }
         }
     }

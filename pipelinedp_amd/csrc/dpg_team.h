@@ -92,18 +92,34 @@ __device__ __forceinline__ bool team_barrier(const TeamSync &ts, uint32_t team, 
     return *sh_ok != 0;
 }
 
+// The histogram-free level 1 (k_scatter's piece mode) leaves level-1 bucket
+// s as 8 pieces, one per XCD region: records [rbase[x F1 + s], + cum[x F1 +
+// s]) for x < 8; tot[s] = their sum, ostart[s] = the bucket's start in the
+// (compact) level-2 output.  Region starts are even (C even).
+struct PieceTab {
+    const int64_t *rbase;
+    const uint32_t *cum;
+    const uint32_t *tot;
+    const uint32_t *ptot;  // the pieces' counts each rounded up to even, summed
+    const int64_t *ostart;
+    uint32_t F1;
+};
+
 // Level 2 over S level-1 buckets (seg_start / seg_cnt; every count <= T *
 // kTeamSub, checked by the host): records of bucket s land in out[seg_start[s],
 // + seg_cnt[s]) grouped by digit (F2 <= kTeamF digits; the scans run over
 // kTeamF, the digits past F2 count 0); base_out[s][d] / tot_out[s][d] = start
 // and count of fine bucket (s, d), d < F2.  gridDim.x = 8 T workgroups, all
-// resident.
-template <class R>
+// resident.  kPc: the buckets are PieceTab pieces (seg_start / seg_cnt
+// unused), read with one 8-byte load per record (a piece may start at an odd
+// record), written compactly from ostart[s].
+template <class R, bool kPc = false>
 __global__ __launch_bounds__(kScatThreads) void k_part2_team(SrcAoS<R> src,
                                                              const int64_t *seg_start,
                                                              const uint32_t *seg_cnt, uint32_t S,
                                                              uint32_t F2, R *out, int64_t *base_out,
-                                                             uint32_t *tot_out, TeamSync ts) {
+                                                             uint32_t *tot_out, TeamSync ts,
+                                                             PieceTab pt = PieceTab{}) {
     constexpr int IPT = kTeamIPT;
     constexpr int SUB = kTeamSub;
     constexpr uint32_t F = kTeamF;
@@ -127,17 +143,21 @@ __global__ __launch_bounds__(kScatThreads) void k_part2_team(SrcAoS<R> src,
     auto elem = [tid](int j) -> uint32_t {
         return (uint32_t)((j >> 1) * 2 * kScatThreads + 2 * tid + (j & 1));
     };
-    // this member's share of bucket s: [st + b0, + lim)
+    // this member's share of bucket s: [st + b0, + lim).  Piece mode: the
+    // share is cut from the bucket's padded index space (every piece rounded
+    // up to an even length, see load_pieces) in even lengths; st is the
+    // bucket's start in the compact output
     auto share = [&](uint32_t s, int64_t &st, uint32_t &n, uint32_t &b0, uint32_t &lim) {
-        n = __builtin_amdgcn_readfirstlane(seg_cnt[s]);
-        const int64_t st0 = seg_start[s];
+        n = __builtin_amdgcn_readfirstlane(kPc ? pt.ptot[s] : seg_cnt[s]);
+        const int64_t st0 = kPc ? pt.ostart[s] : seg_start[s];
         st = (int64_t)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)st0 >> 32)) << 32) |
                        (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)st0));
-        const uint32_t q = (n + T - 1) / T;
+        const uint32_t q = kPc ? (((n + T - 1) / T + 1) & ~1u) : (n + T - 1) / T;
         b0 = min(n, m * q);
         lim = min(n, b0 + q) - b0;  // <= SUB (host check)
     };
     R rec[IPT];
+    uint32_t vmask = ~0u;  // piece mode: bit j = element j is a record (not padding)
     // loads of a share (unconditional, clamped into it: a guarded load would
     // serialise them); a member past the bucket's end loads nothing
     auto load = [&](int64_t base, uint32_t lim) {
@@ -156,6 +176,55 @@ __global__ __launch_bounds__(kScatThreads) void k_part2_team(SrcAoS<R> src,
             for (int j = 0; j < IPT; ++j) rec[j] = lim ? src.fetch(base) : R{};
         }
     };
+    // piece mode: the bucket's index space lists its 8 pieces in order, each
+    // padded to an even length (ppre: padded exclusive prefix), so an even
+    // index and its successor lie in one piece at an even offset -- one
+    // 16-byte load (region starts are even: C is even); the padding slot
+    // after an odd piece is loaded from inside the region and masked out.
+    // Offsets are 32-bit from the bucket's first region (the bucket's
+    // regions span 8 C records).
+    auto load_pieces = [&](uint32_t s, uint32_t b0, uint32_t lim) {
+        uint32_t ppre[8], dl[8], pc[8];
+        const int64_t rb0 = pt.rbase[s];
+        const int64_t base0 = (int64_t)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)rb0 >> 32)) << 32) |
+                                        (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)rb0));
+        uint32_t acc = 0;
+#pragma unroll
+        for (int p = 0; p < 8; ++p) {
+            const uint32_t off = __builtin_amdgcn_readfirstlane(
+                (uint32_t)(pt.rbase[(size_t)p * pt.F1 + s] - rb0));
+            pc[p] = __builtin_amdgcn_readfirstlane(pt.cum[(size_t)p * pt.F1 + s]);
+            ppre[p] = acc;
+            dl[p] = off - acc;  // index i of piece p sits at base0 + i + dl[p] (mod 2^32)
+            acc += (pc[p] + 1u) & ~1u;
+        }
+        const char *bp = reinterpret_cast<const char *>(src.a + base0);
+        uint32_t vm = 0;
+#pragma unroll
+        for (int mm = 0; mm < IPT / 2; ++mm) {
+            const uint32_t o = mm * 2 * kScatThreads + 2 * tid;
+            const uint32_t i = b0 + min(o, lim - 2);  // even (b0, lim even)
+            uint32_t d = dl[0], c = pc[0] + ppre[0];
+#pragma unroll
+            for (int p = 1; p < 8; ++p) {
+                const bool in = i >= ppre[p];
+                d = in ? dl[p] : d;
+                c = in ? pc[p] + ppre[p] : c;  // end of the piece's records
+            }
+            R x0, x1;
+            const uint32_t boff = (i + d) * (uint32_t)sizeof(R);
+            static_assert(sizeof(R) == 8, "piece-mode teams read 8-byte records");
+            const u64x2 w = *reinterpret_cast<const u64x2 *>(bp + boff);
+            const uint64_t w0 = w.x, w1 = w.y;
+            __builtin_memcpy(&x0, &w0, sizeof(R));
+            __builtin_memcpy(&x1, &w1, sizeof(R));
+            rec[2 * mm] = x0;
+            rec[2 * mm + 1] = x1;
+            vm |= (i < c ? 1u : 0u) << (2 * mm);
+            vm |= (i + 1 < c ? 1u : 0u) << (2 * mm + 1);
+        }
+        vmask = vm;
+    };
     uint32_t k = 0;  // buckets done = team barriers passed
     for (uint32_t s = team; s < S; s += 8) {
         int64_t st;
@@ -171,14 +240,21 @@ __global__ __launch_bounds__(kScatThreads) void k_part2_team(SrcAoS<R> src,
         }
         uint32_t *tt = ts.tot + ((size_t)team * 3 + k % 3) * F;
         // ---- load + rank
-        load(st + b0, lim);
+        if constexpr (kPc) {
+            vmask = 0;
+            if (lim > 0) load_pieces(s, b0, lim);
+        } else {
+            load(st + b0, lim);
+        }
         uint32_t dr[IPT];
+        uint32_t nv = 0;  // records of the share (lim less the padding)
         {
             uint32_t dg[IPT];
             bool okv[IPT];
 #pragma unroll
             for (int j = 0; j < IPT; ++j) {
                 okv[j] = elem(j) < lim;
+                if constexpr (kPc) okv[j] = okv[j] && ((vmask >> j) & 1u);
                 dg[j] = okv[j] ? src.digit(rec[j]) : 0u;
             }
             uint32_t rk[IPT];
@@ -202,8 +278,10 @@ __global__ __launch_bounds__(kScatThreads) void k_part2_team(SrcAoS<R> src,
             if (lane == 63) sh16[wv] = wt;
             __syncthreads();
 #pragma unroll
-            for (int w = 0; w < kScatThreads / 64; ++w)
+            for (int w = 0; w < kScatThreads / 64; ++w) {
                 if (w < wv) e += sh16[w];
+                nv += sh16[w];
+            }
 #pragma unroll
             for (int u = 0; u < DPT; ++u) {
                 dstart[d0 + u] = e;
@@ -211,7 +289,7 @@ __global__ __launch_bounds__(kScatThreads) void k_part2_team(SrcAoS<R> src,
                 cnt[d0 + u] = 0;
                 e += c[u];
             }
-            if (tid == 0) dstart[F] = lim;
+            if (tid == 0) dstart[F] = nv;
         }
         ++k;
         if (!team_barrier(ts, team, T * k, &sh_ok)) return;
@@ -255,12 +333,12 @@ __global__ __launch_bounds__(kScatThreads) void k_part2_team(SrcAoS<R> src,
         // (loading the next bucket's share during the write-out measured
         // slower: 5.2 -> 5.65 ms at config 2, 128 VGPRs with spills)
         constexpr int WB = 4;
-        for (uint32_t k0 = 0; k0 < lim; k0 += WB * kScatThreads) {
+        for (uint32_t k0 = 0; k0 < nv; k0 += WB * kScatThreads) {
             W x[WB];
             uint32_t dd[WB], kc[WB];
 #pragma unroll
             for (int u = 0; u < WB; ++u) {
-                kc[u] = min(k0 + u * kScatThreads + tid, lim - 1);
+                kc[u] = min(k0 + u * kScatThreads + tid, nv - 1);
                 x[u] = stage[kc[u]];
                 dd[u] = src.digit(from_words<R>(x[u]));
             }

@@ -93,25 +93,52 @@ def test_config2_bounding_triggered_matches_oracle(built, config2_data):
     assert np.allclose(out.values.cpu().numpy()[np.argsort(gid)], o[ids], rtol=1e-12, atol=1e-6)
 
 
-@pytest.mark.parametrize("mode", ["team", "grouped", "team_abort"])
+@pytest.mark.parametrize("mode", ["pieces", "team", "grouped", "team_abort", "piece_overflow"])
 def test_config2_level2_paths_match_oracle(built, config2_data, monkeypatch, mode):
-    """Level 2 three ways, every one bit-exact against the oracle (kept pairs,
-    counts; sums to 1e-9): the team kernel without a histogram pass
-    (dpg_team.h, the default for 8-byte records), the grouped histogram path
-    (DPG_TEAM_L2=0), and a team whose barrier gives up (test hook
-    DPG_DEBUG_TEAM_ABORT: abort flag + err bit 8, as after a timeout), which
-    the host detects at the chunking sync and redoes with the histogram path."""
+    """The first two partition levels five ways, every one bit-exact against
+    the oracle (kept pairs, counts; sums to 1e-9):
+    team -- the default for 8-byte records: level 1 with its histogram,
+      level 2 by teams without one;
+    pieces -- level 1 without a histogram pass too (DPG_L1_PIECES=1:
+      per-XCD fixed-capacity regions, k_scatter's piece mode), level 2 by
+      teams reading the pieces;
+    grouped -- both levels with histograms (DPG_TEAM_L2=0);
+    team_abort -- pieces, and a team barrier that gives up (test hook
+      DPG_DEBUG_TEAM_ABORT: abort flag + err bit 8, as after a timeout); the
+      host sees it at the chunking sync and redoes both levels with the
+      histogram paths;
+    piece_overflow -- pieces in regions far too small
+      (DPG_DEBUG_PIECE_CAP=64): runs go to the dump area, err bit 16, and
+      the host redoes level 1 with its histogram before level 2."""
     if mode == "grouped":
         monkeypatch.setenv("DPG_TEAM_L2", "0")
+    if mode in ("pieces", "team_abort", "piece_overflow"):
+        monkeypatch.setenv("DPG_L1_PIECES", "1")
     if mode == "team_abort":
         monkeypatch.setenv("DPG_DEBUG_TEAM_ABORT", "1")
+    if mode == "piece_overflow":
+        monkeypatch.setenv("DPG_DEBUG_PIECE_CAP", "64")
     pid, pk, val = config2_data
     res, _, got = _run(pid, pk, val, _c2_params(8, 2), P2)
     ref = oracle.bound_aggregate(pid, pk, val, res.last_bound_fields, SEED)
     _assert_partials(got, ref)
     stages = res.backend.ctx.stage_times()
+    assert ("partition1:pieces" in stages) == (mode in ("pieces", "team_abort", "piece_overflow"))
+    assert ("partition1:hist" in stages) == (mode != "pieces")
     assert ("partition2:team" in stages) == (mode != "grouped")
-    assert ("partition2:hist" in stages) == (mode != "team")
+    assert ("partition2:hist" in stages) == (mode in ("grouped", "team_abort"))
+
+
+def test_config2_pieces_range_error(built, config2_data, monkeypatch):
+    """The histogram-free level 1 checks whole privacy ids itself: an id past
+    the declared range (high word differs, low word in range) fails the
+    call with the key-range error, as the histogram path does."""
+    monkeypatch.setenv("DPG_L1_PIECES", "1")
+    pid, pk, val = config2_data
+    bad = pid.copy()
+    bad[123457] += 1 << 32
+    with pytest.raises(Exception, match="range"):
+        _run(bad, pk, val, _c2_params(8, 2), P2, pid_range=(0, U2))
 
 
 # ------------------------------------------------------------------ config 4
