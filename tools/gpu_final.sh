@@ -20,4 +20,6 @@ timeout -k 10 400 python bench.py --workload config4 --public --steps 4 --warmup
 python -c "import json; d=json.load(open('$O/bench_c4p.json')); print('c4 public ms', round(d['ms_per_step'],2))"
 timeout -k 10 400 python bench.py --workload config5 --steps 3 --warmup 1 > $O/bench_c5.json 2> $O/bench_c5.err || { echo c5 failed; tail -20 $O/bench_c5.err; exit 1; }
 python -c "import json; d=json.load(open('$O/bench_c5.json')); print('c5 ms', round(d['ms_per_step'],2), d['stage_ms']); print(d.get('cpu_baseline'))"
+timeout -k 10 300 python -u tools/ua_timing.py > $O/ua_timing.log 2>&1 || { echo ua_timing failed; tail -5 $O/ua_timing.log; exit 1; }
+tail -2 $O/ua_timing.log
 echo done
