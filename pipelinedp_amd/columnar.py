@@ -168,6 +168,26 @@ def _device_bitmap(ids: torch.Tensor, P: int, device) -> Tuple[torch.Tensor, int
     return mask.contiguous(), count
 
 
+def _range_bitmap(lo: int, hi: int, P: int, device) -> Tuple[torch.Tensor, int]:
+    """The _device_bitmap of range(lo, hi) without materialising the ids
+    (config 4's public_partitions = range(1e8): 800 MB of ids, a scatter
+    and two reductions per release otherwise)."""
+    mask = torch.zeros((P + 7) // 8, dtype=torch.uint8, device=device)
+    if hi <= lo:
+        return mask, 0
+    _check_public_range(lo, hi - 1, P)
+    b0, b1 = lo >> 3, (hi - 1) >> 3
+    head = (0xFF << (lo & 7)) & 0xFF
+    tail = 0xFF >> (7 - ((hi - 1) & 7))
+    if b0 == b1:
+        mask[b0] = head & tail
+    else:
+        mask[b0] = head
+        mask[b0 + 1:b1] = 0xFF
+        mask[b1] = tail
+    return mask, hi - lo
+
+
 def _range(t: torch.Tensor):
     if t.numel() == 0:
         return 0, -1
@@ -202,10 +222,14 @@ def encode(col, extractors, device: torch.device, need_values: bool,
     # dense integer keys with a declared P and array-like public partitions:
     # the public bitmap is built on the device (config 4: 1e8 public ids)
     pub_dense = None
+    pub_range = None  # a unit-step range: its bitmap is two partial bytes and a fill
     if public_partitions is not None and hint is not None and _integer_like(pk):
-        pub_dense = _public_id_tensor(public_partitions, device)
+        if isinstance(public_partitions, range) and public_partitions.step == 1:
+            pub_range = (public_partitions.start, public_partitions.stop)
+        else:
+            pub_dense = _public_id_tensor(public_partitions, device)
     public_list = (None if public_partitions is None or pub_dense is not None
-                   else list(public_partitions))
+                   or pub_range is not None else list(public_partitions))
     key_table = None
     pk_ids = None
     public_ids = None
@@ -276,7 +300,9 @@ def encode(col, extractors, device: torch.device, need_values: bool,
                        n_partitions=int(P), key_table=key_table, pid_min=pid_min,
                        pid_count=pid_count, rec_id_offset=rec_off,
                        partitions_declared=hint is not None and key_table is None)
-    if pub_dense is not None:
+    if pub_range is not None:
+        enc.public_mask, enc.public_count = _range_bitmap(*pub_range, int(P), device)
+    elif pub_dense is not None:
         enc.public_mask, enc.public_count = _device_bitmap(pub_dense, int(P), device)
     elif public_ids is not None:
         mask = np.zeros((P + 7) // 8, dtype=np.uint8)

@@ -282,30 +282,45 @@ __device__ __forceinline__ double granularity(double scale) {
     return exp2(ceil(log2(scale * 0x1.0p-40)));
 }
 
+// The lattice of a noise scale: g = granularity(scale) and its exact
+// reciprocal (g is a power of two, so x * ig == x / g bit for bit).  The
+// select / noise kernel computes it once per scale and thread instead of a
+// log2 / exp2 pair per partition.
+struct Gran {
+    double g, ig;
+};
+__device__ __forceinline__ Gran gran_of(double scale) {
+    if (!(scale > 0)) return Gran{0.0, 0.0};
+    const double g = granularity(scale);
+    return Gran{g, 1.0 / g};
+}
+
 // x + Laplace(b), snapped to the granularity lattice (see oracle dpo_laplace)
-__device__ __forceinline__ double laplace_noise(double x, double b, const uint32_t u[4]) {
+__device__ __forceinline__ double laplace_noise(double x, double b, const uint32_t u[4],
+                                                const Gran &G) {
     if (!(b > 0)) return x;
-    double g = granularity(b);
+    const double bg = b * G.ig;
     double e1 = -log(u53(u[0], u[1]));
     double e2 = -log(u53(u[2], u[3]));
-    double k = floor(e1 * (b / g)) - floor(e2 * (b / g));
-    return rint(x / g) * g + k * g;
+    double k = floor(e1 * bg) - floor(e2 * bg);
+    return rint(x * G.ig) * G.g + k * G.g;
 }
 
-__device__ __forceinline__ double gaussian_noise(double x, double sigma, const uint32_t u[4]) {
+__device__ __forceinline__ double gaussian_noise(double x, double sigma, const uint32_t u[4],
+                                                 const Gran &G) {
     if (!(sigma > 0)) return x;
-    double g = granularity(sigma);
     double r = sqrt(-2.0 * log(u53(u[0], u[1])));
     double z = r * cos(6.283185307179586476925286766559 * u53(u[2], u[3]));
-    return rint(x / g) * g + rint(sigma * z / g) * g;
+    return rint(x * G.ig) * G.g + rint(sigma * z * G.ig) * G.g;
 }
 
-__device__ __forceinline__ double add_noise(int kind, double x, double scale, uint64_t seed,
-                                            uint64_t pk, uint32_t slot) {
+__device__ __forceinline__ double add_noise(int kind, double x, double scale, const Gran &G,
+                                            uint64_t seed, uint64_t pk, uint32_t slot) {
     if (kind == DPG_NOISE_NONE) return x;
     uint32_t c[4] = {(uint32_t)pk, (uint32_t)(pk >> 32), slot, 0u};
     philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32) ^ DPG_TAG_NOISE);
-    return kind == DPG_NOISE_GAUSSIAN ? gaussian_noise(x, scale, c) : laplace_noise(x, scale, c);
+    return kind == DPG_NOISE_GAUSSIAN ? gaussian_noise(x, scale, c, G)
+                                      : laplace_noise(x, scale, c, G);
 }
 
 __device__ __forceinline__ void select_uniforms(uint64_t seed, uint64_t pk, uint32_t c[4]) {

@@ -143,7 +143,8 @@ struct NoiseArgs {
 };
 
 __device__ __forceinline__ bool keep_partition(const SelectArgs &s, uint64_t seed, uint64_t gk,
-                                               int64_t local, int64_t rows, const double *tab) {
+                                               int64_t local, int64_t rows, const double *tab,
+                                               const Gran &sg) {
     if (s.strategy == DPG_SELECT_NONE)
         return s.public_mask ? ((s.public_mask[local >> 3] >> (local & 7)) & 1) : true;
     if (rows <= 0) return false;  // partitions absent from the data
@@ -159,8 +160,8 @@ __device__ __forceinline__ bool keep_partition(const SelectArgs &s, uint64_t see
         return u53(u[0], u[1]) < pr;
     }
     if (s.strategy == DPG_SELECT_LAPLACE_THRESHOLD)
-        return laplace_noise((double)n, s.noise_scale, u) > s.threshold;
-    return gaussian_noise((double)n, s.noise_scale, u) > s.threshold;
+        return laplace_noise((double)n, s.noise_scale, u, sg) > s.threshold;
+    return gaussian_noise((double)n, s.noise_scale, u, sg) > s.threshold;
 }
 
 // _select_private_partitions_internal (dp_engine.py:305-361) fused with
@@ -177,11 +178,16 @@ __global__ __launch_bounds__(256) void k_select_noise(const int64_t *rows, const
         __syncthreads();
     }
     const double *tab = lds_tab ? s_tab : s.table;
+    // lattices of the selection noise and of each metric slot, per thread
+    const Gran sg = gran_of(s.noise_scale);
+    Gran G[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) G[q] = gran_of(z.scale[q]);
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < P;
          k += (int64_t)gridDim.x * blockDim.x) {
         const uint64_t gk = (uint64_t)(s.pk_offset + k * s.pk_stride);
         const int64_t r = rows[k];
-        const bool kp = keep_partition(s, seed, gk, k, r, tab);
+        const bool kp = keep_partition(s, seed, gk, k, r, tab, sg);
         keep[k] = kp ? 1 : 0;
         double *o = out + k * z.n_out;
         if (!kp) {
@@ -193,14 +199,14 @@ __global__ __launch_bounds__(256) void k_select_noise(const int64_t *rows, const
         const int kind = z.kind;
         if (z.family == DPG_FAMILY_VARIANCE) {
             // dp_computations.py:307-366
-            double dc = add_noise(kind, cnt, z.scale[DPG_SLOT_COUNT], seed, gk, DPG_SLOT_COUNT);
+            double dc = add_noise(kind, cnt, z.scale[DPG_SLOT_COUNT], G[DPG_SLOT_COUNT], seed, gk, DPG_SLOT_COUNT);
             double den = dc > 1.0 ? dc : 1.0;
             double mean = z.mean_const ? z.mean_const_value
                                        : add_noise(kind, nsum ? nsum[k] : 0.0,
-                                                   z.scale[DPG_SLOT_SUM], seed, gk,
+                                                   z.scale[DPG_SLOT_SUM], G[DPG_SLOT_SUM], seed, gk,
                                                    DPG_SLOT_SUM) / den;
             double msq = z.msq_const ? z.msq_const_value
-                                     : add_noise(kind, nsq ? nsq[k] : 0.0, z.scale[DPG_SLOT_NSQ],
+                                     : add_noise(kind, nsq ? nsq[k] : 0.0, z.scale[DPG_SLOT_NSQ], G[DPG_SLOT_NSQ],
                                                  seed, gk, DPG_SLOT_NSQ) / den;
             double var = msq - mean * mean;
             if (!z.mean_const) mean += z.mid;
@@ -210,8 +216,8 @@ __global__ __launch_bounds__(256) void k_select_noise(const int64_t *rows, const
             V[DPG_V_MEAN] = mean;
         } else if (z.family == DPG_FAMILY_MEAN) {
             // dp_computations.py:563-569
-            double dc = add_noise(kind, cnt, z.scale[DPG_SLOT_COUNT], seed, gk, DPG_SLOT_COUNT);
-            double dn = add_noise(kind, nsum ? nsum[k] : 0.0, z.scale[DPG_SLOT_SUM], seed, gk,
+            double dc = add_noise(kind, cnt, z.scale[DPG_SLOT_COUNT], G[DPG_SLOT_COUNT], seed, gk, DPG_SLOT_COUNT);
+            double dn = add_noise(kind, nsum ? nsum[k] : 0.0, z.scale[DPG_SLOT_SUM], G[DPG_SLOT_SUM], seed, gk,
                                   DPG_SLOT_SUM);
             double mean = z.mid + dn / (dc > 1.0 ? dc : 1.0);
             V[DPG_V_COUNT] = dc;
@@ -220,14 +226,14 @@ __global__ __launch_bounds__(256) void k_select_noise(const int64_t *rows, const
         } else {
             if (z.slot_mask & (1u << DPG_SLOT_COUNT))
                 V[DPG_V_COUNT] =
-                    add_noise(kind, cnt, z.scale[DPG_SLOT_COUNT], seed, gk, DPG_SLOT_COUNT);
+                    add_noise(kind, cnt, z.scale[DPG_SLOT_COUNT], G[DPG_SLOT_COUNT], seed, gk, DPG_SLOT_COUNT);
             if (z.slot_mask & (1u << DPG_SLOT_SUM))
-                V[DPG_V_SUM] = add_noise(kind, sum ? sum[k] : 0.0, z.scale[DPG_SLOT_SUM], seed,
+                V[DPG_V_SUM] = add_noise(kind, sum ? sum[k] : 0.0, z.scale[DPG_SLOT_SUM], G[DPG_SLOT_SUM], seed,
                                          gk, DPG_SLOT_SUM);
         }
         if (z.slot_mask & (1u << DPG_SLOT_PID))
             V[DPG_V_PRIVACY_ID_COUNT] =
-                add_noise(kind, (double)r, z.scale[DPG_SLOT_PID], seed, gk, DPG_SLOT_PID);
+                add_noise(kind, (double)r, z.scale[DPG_SLOT_PID], G[DPG_SLOT_PID], seed, gk, DPG_SLOT_PID);
         for (int j = 0; j < z.n_out; ++j) o[j] = V[z.out_src[j]];
     }
 }

@@ -5,6 +5,7 @@ sampling_utils.py:32-51 ValueSampler hashes repr(key))."""
 import hashlib
 
 import numpy as np
+import pytest
 import torch
 
 from pipelinedp_amd import aggregate_params as agg
@@ -64,3 +65,22 @@ def test_numpy_scalar_row_keys_come_back_as_given():
     # plain Python integer rows stay dense ids decoded as Python ints
     enc2 = columnar.encode([(1, 5, 1.0), (2, 9, 2.0)], ex, torch.device("cpu"), True)
     assert enc2.key_table is None
+
+
+@pytest.mark.parametrize("lo,hi,P", [(0, 100, 100), (3, 4, 10), (5, 13, 20), (8, 16, 16),
+                                     (0, 0, 9), (7, 9, 9), (1, 1000, 1003), (16, 17, 40)])
+def test_range_bitmap_matches_ids_bitmap(lo, hi, P):
+    """public_partitions = range(lo, hi) builds its bitmap without listing
+    the ids; it must equal the bitmap of the listed ids bit for bit."""
+    from pipelinedp_amd import columnar
+    dev = torch.device("cpu")
+    got, n = columnar._range_bitmap(lo, hi, P, dev)
+    want, m = columnar._device_bitmap(torch.arange(lo, hi, dtype=torch.int64), P, dev)
+    assert n == m == max(0, hi - lo)
+    assert torch.equal(got, want)
+
+
+def test_range_bitmap_rejects_out_of_range():
+    from pipelinedp_amd import columnar
+    with pytest.raises(ValueError, match="outside"):
+        columnar._range_bitmap(0, 11, 10, torch.device("cpu"))
