@@ -1942,8 +1942,15 @@ int dpg_utility_analysis(dpg_ctx *ctx, const dpg_pair_entry *pairs,
     if (n > 0) {
         const int64_t runs = (n + kUaRun - 1) / kUaRun;
         if (runs >= 0x7FFFFFFF) return fail(ctx, DPG_ERR_UNSUPPORTED, "too many pairs");
-        k_ua_accumulate<<<(unsigned)runs, 64, 0, s>>>(reinterpret_cast<const ItemPA *>(pairs),
-                                                      partition_start, n, a);
+        using AccK = void (*)(const ItemPA *, const int64_t *, int64_t, UaArgs);
+        static const AccK acc_k[8] = {
+            k_ua_accumulate<false, false, false>, k_ua_accumulate<false, false, true>,
+            k_ua_accumulate<false, true, false>,  k_ua_accumulate<false, true, true>,
+            k_ua_accumulate<true, false, false>,  k_ua_accumulate<true, false, true>,
+            k_ua_accumulate<true, true, false>,   k_ua_accumulate<true, true, true>};
+        const AccK kern = acc_k[(a.has_sum ? 4 : 0) | (a.has_count ? 2 : 0) | (a.has_pid ? 1 : 0)];
+        kern<<<(unsigned)runs, 64, 0, s>>>(reinterpret_cast<const ItemPA *>(pairs),
+                                           partition_start, n, a);
         LAUNCH_CHECK();
     }
     if (u->public_partitions) {

@@ -97,6 +97,10 @@ __device__ __forceinline__ void ua_put(double *dst, double v, bool atomic) {
     else *dst = v;
 }
 
+// kSum / kCount / kPid: the metrics of the sweep (a.has_*), as template
+// flags so that the loop holds neither their branches nor the selects the
+// compiler if-converts them into.
+template <bool kSum, bool kCount, bool kPid>
 __global__ __launch_bounds__(64) void k_ua_accumulate(const ItemPA *pairs,
                                                       const int64_t *pstart, int64_t n,
                                                       UaArgs a) {
@@ -113,19 +117,22 @@ __global__ __launch_bounds__(64) void k_ua_accumulate(const ItemPA *pairs,
     // PRIVACY_ID_COUNT's (x = 1 for count > 0) follow from the moments at the
     // flush: total rn - nz, l0 terms -(sum of 1 - p) = e - rn and sum of q =
     // v, corrected by the pairs of count 0 (pre-aggregated input only).
-    // FP64 arithmetic is what bounds this loop (half the FP32 vector rate;
-    // config 5: ~7e8 pairs x 64 configurations), so the integer terms stay
-    // integers (pairs and records per partition, COUNT's clip-to-max error)
-    // and the float ones use min / max / fma forms (same values, fewer
+    // The loop is VALU-issue bound (config 5: ~7e8 pairs, one wave64
+    // instruction per term for all 64 configurations; ~37 instructions per
+    // pair), so every term costs instructions, not bytes: the pair and
+    // record counts stay wave-uniform scalars, COUNT's clip-to-max error is
+    // the exact double sum of the clipped counts less the record count, and
+    // the float terms use min / max / fma forms (same values, fewer
     // instructions than compare-and-select chains).
     double e = 0, v = 0, t = 0;
     uint32_t rn = 0;                   // pairs of the partition (wave-uniform)
     uint64_t rc = 0;                   // records of the partition (wave-uniform)
     ErrAcc es;
-    int64_t cmx = 0;                   // COUNT: clip-to-max error (integer)
+    double spci = 0;                   // COUNT: sum of the clipped counts (exact: < 2^53)
     double cel = 0, cvl = 0;           // COUNT: l0 mean, l0 variance
     double nz = 0, zel = 0, zvl = 0;   // pairs of count 0: number, sum 1 - p, sum q
     const uint32_t mcpp_i = cf.mcpp >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)cf.mcpp;
+    const double clo = cf.lo, chi = cf.hi;
     es.clear();
     uint32_t cur = pairs[lo].pk;
     bool skip = a.sample_mask && !bit_of(a.sample_mask, cur);
@@ -159,9 +166,10 @@ __global__ __launch_bounds__(64) void k_ua_accumulate(const ItemPA *pairs,
             ua_put(o + 4 * C64, vl0, atomic);
             o += 5 * C64;
         };
-        if (a.has_sum) put5(es.tot, es.cmin, es.cmax, es.el0, es.vl0);
-        if (a.has_count) put5(rcd, 0.0, (double)cmx, cel, cvl);
-        if (a.has_pid) put5(rnd - nz, 0.0, 0.0, (e - rnd) + zel, v - zvl);
+        if (kSum) put5(es.tot, es.cmin, es.cmax, es.el0, es.vl0);
+        // clip-to-max error sum(min(cnt, mcpp) - cnt) = spci - rc, exact
+        if (kCount) put5(rcd, 0.0, spci - rcd, cel, cvl);
+        if (kPid) put5(rnd - nz, 0.0, 0.0, (e - rnd) + zel, v - zvl);
     };
     // The 64 pairs of a block are broadcast to the configurations through
     // LDS (uniform-address reads), not by readlane of the loaded registers:
@@ -189,7 +197,7 @@ __global__ __launch_bounds__(64) void k_ua_accumulate(const ItemPA *pairs,
                 rn = 0;
                 rc = 0;
                 es.clear();
-                cmx = 0;
+                spci = 0.0;
                 cel = cvl = 0.0;
                 nz = zel = zvl = 0.0;
                 cur = pk;
@@ -207,23 +215,23 @@ __global__ __launch_bounds__(64) void k_ua_accumulate(const ItemPA *pairs,
             t = fma(q, fma(-2.0, p, 1.0), t);
             rn += 1;
             rc += cnt;
-            if (a.has_sum) {
+            if constexpr (kSum) {
                 const double x = s_sum[j];
-                const double pc = fmin(fmax(x, cf.lo), cf.hi);
+                const double pc = fmin(fmax(x, clo), chi);
                 es.tot += x;
-                es.cmin += fmax(cf.lo - x, 0.0);  // pc - x where x < lo
-                es.cmax += fmin(cf.hi - x, 0.0);  // pc - x where x > hi
+                es.cmin += fmax(clo - x, 0.0);  // pc - x where x < lo
+                es.cmax += fmin(chi - x, 0.0);  // pc - x where x > hi
                 es.el0 = fma(-pc, omp, es.el0);
                 es.vl0 = fma(pc * pc, q, es.vl0);
             }
-            if (a.has_count) {
+            if constexpr (kCount) {
                 const uint32_t pci = cnt < mcpp_i ? cnt : mcpp_i;
                 const double pc = (double)pci;
-                cmx += (int64_t)pci - (int64_t)cnt;
+                spci += pc;
                 cel = fma(-pc, omp, cel);
                 cvl = fma(pc * pc, q, cvl);
             }
-            if (a.has_pid && cnt == 0) {  // wave-uniform (the pair is broadcast)
+            if (kPid && cnt == 0) {  // wave-uniform (the pair is broadcast)
                 nz += 1.0;
                 zel += omp;
                 zvl += q;
