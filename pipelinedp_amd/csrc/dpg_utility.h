@@ -92,6 +92,18 @@ struct ErrAcc {
     }
 };
 
+// min(max(x, lo), hi) as two bare VALU instructions.  fmin / fmax lower to
+// the same v_max_f64 / v_min_f64 but, in the kernels' IEEE mode, first
+// canonicalise every operand the compiler cannot prove canonical (here x,
+// lo and hi: three more FP64 instructions per pair and configuration in
+// k_ua_accumulate).  The operands are never signalling NaNs (values and
+// bounds come from finite host data), for which the result is the same.
+__device__ __forceinline__ double clamp_f64(double x, double lo, double hi) {
+    double r;
+    asm("v_max_f64 %0, %1, %2\n\tv_min_f64 %0, %0, %3" : "=&v"(r) : "v"(x), "v"(lo), "v"(hi));
+    return r;
+}
+
 __device__ __forceinline__ void ua_put(double *dst, double v, bool atomic) {
     if (atomic) atomicAdd(dst, v);
     else *dst = v;
@@ -217,7 +229,7 @@ __global__ __launch_bounds__(64) void k_ua_accumulate(const ItemPA *pairs,
             rc += cnt;
             if constexpr (kSum) {
                 const double x = s_sum[j];
-                const double pc = fmin(fmax(x, clo), chi);
+                const double pc = clamp_f64(x, clo, chi);
                 es.tot += x;
                 es.cmin += fmax(clo - x, 0.0);  // pc - x where x < lo
                 es.cmax += fmin(chi - x, 0.0);  // pc - x where x > hi
