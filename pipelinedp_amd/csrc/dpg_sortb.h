@@ -225,17 +225,35 @@ __device__ __forceinline__ void bitonic_sort(uint64_t (&k)[E], uint32_t (&o)[E])
 }
 
 // The same network over keys alone (unique keys: the candidate position
-// rides in the low bits, see sort_chunk).
+// rides in the low bits, see sort_chunk), on keys that are finite positive
+// normal doubles when read as float64 (bit 63 clear, bits 62..61 = 01, see sort_chunk's packed
+// keys; padding +inf): for those, float64 order is the unsigned order of the
+// bits, so a compare-exchange is one v_min_f64 and one v_max_f64 (bare, in
+// inline asm: fmin / fmax would first canonicalise both operands) instead of
+// a 64-bit compare and four selects.
+__device__ __forceinline__ uint64_t fmin_bits(uint64_t a, uint64_t b) {
+    double x = __builtin_bit_cast(double, a), y = __builtin_bit_cast(double, b), r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
+    return __builtin_bit_cast(uint64_t, r);
+}
+__device__ __forceinline__ uint64_t fmax_bits(uint64_t a, uint64_t b) {
+    double x = __builtin_bit_cast(double, a), y = __builtin_bit_cast(double, b), r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
+    return __builtin_bit_cast(uint64_t, r);
+}
+constexpr uint64_t kSkPadF = 0x7FF0000000000000ull;  // +inf: above every packed key
+constexpr uint64_t kSkTagF = 1ull << 61;              // exponent bits 01...: normal, finite
+
 template <int E>
-__device__ __forceinline__ void bitonic_sort_keys(uint64_t (&k)[E]) {
+__device__ __forceinline__ void bitonic_sort_keys_f64(uint64_t (&k)[E]) {
     constexpr int LOG_S = E == 1 ? 6 : E == 2 ? 7 : E == 4 ? 8 : 9;
     constexpr int LOG_E = LOG_S - 6;
     uint32_t lid = __lane_id();
     asm volatile("" : "+v"(lid));
     auto cex = [&](int j, int j2) {
         const uint64_t a = k[j], b = k[j2];
-        k[j] = a < b ? a : b;
-        k[j2] = a < b ? b : a;
+        k[j] = fmin_bits(a, b);
+        k[j2] = fmax_bits(a, b);
     };
 #pragma unroll
     for (int lk = 1; lk <= LOG_S; ++lk) {
@@ -253,10 +271,8 @@ __device__ __forceinline__ void bitonic_sort_keys(uint64_t (&k)[E]) {
 #pragma unroll
             for (int j = 0; j < E; ++j) y[j] = xlane64(k[E - 1 - j], m);
 #pragma unroll
-            for (int j = 0; j < E; ++j) {
-                const bool take = lower ? y[j] < k[j] : k[j] < y[j];
-                k[j] = take ? y[j] : k[j];
-            }
+            for (int j = 0; j < E; ++j)
+                k[j] = lower ? fmin_bits(k[j], y[j]) : fmax_bits(k[j], y[j]);
         }
 #pragma unroll
         for (int ls = lk - 2; ls >= 0; --ls) {
@@ -271,8 +287,7 @@ __device__ __forceinline__ void bitonic_sort_keys(uint64_t (&k)[E]) {
 #pragma unroll
                 for (int j = 0; j < E; ++j) {
                     const uint64_t y = xlane64(k[j], m);
-                    const bool take = lower ? y < k[j] : k[j] < y;
-                    k[j] = take ? y : k[j];
+                    k[j] = lower ? fmin_bits(k[j], y) : fmax_bits(k[j], y);
                 }
             }
         }
@@ -338,15 +353,16 @@ __device__ __forceinline__ int sort_chunk(uint32_t nc, char *smem, const BoundPa
     full[lane + 64u] = 0;
     bool sorted_packed = false;
     if constexpr (!kWPk && !kLex && E <= 4 && DPG_SORT_PACKED) {
-        // keys alone (5 instead of 7 VALU per compare-exchange): pid slot (7
-        // bits) | top 48 - pkbits bits of the pair priority | pk | candidate
-        // position (9 bits); the full keys and record indices are read back
-        // by position.  Two pairs of one pid whose priorities agree in the
-        // kept bits (~24^2 / 2^29 per pid at pkbits 20) may come out in pk
-        // order instead of priority order: the full keys are then not
-        // ascending and the chunk is sorted again with key and payload.
+        // keys alone (2 VALU per in-lane compare-exchange, see
+        // bitonic_sort_keys_f64): tag bits 01 | pid slot (7 bits) | top 45 -
+        // pkbits bits of the pair priority | pk | candidate position (9
+        // bits); the full keys and record indices are read back by position.
+        // Two pairs of one pid whose priorities agree in the kept bits (~24^2
+        // / 2^26 per pid at pkbits 20) may come out in pk order instead of
+        // priority order: the full keys are then not ascending and the chunk
+        // is sorted again with key and payload.
         const uint32_t pkb = f.pkbits;
-        const uint32_t ppb = 48u - pkb;
+        const uint32_t ppb = 45u - pkb;
         const uint64_t pkm = (1ull << pkb) - 1ull;
         uint64_t pk64[E];
 #pragma unroll
@@ -354,11 +370,11 @@ __device__ __forceinline__ int sort_chunk(uint32_t nc, char *smem, const BoundPa
             const uint32_t i = lane * E + j;
             const uint64_t x = k[j];
             const uint64_t pp = (x >> kSkPkBits) & 0xFFFFFFFFull;
-            pk64[j] = i < nc ? (((x >> 56) << 57) | ((pp >> (32u - ppb)) << (9u + pkb)) |
+            pk64[j] = i < nc ? (kSkTagF | ((x >> 56) << 54) | ((pp >> (32u - ppb)) << (9u + pkb)) |
                                 ((x & pkm) << 9) | (uint64_t)i)
-                             : kSkPad;
+                             : kSkPadF;
         }
-        bitonic_sort_keys<E>(pk64);
+        bitonic_sort_keys_f64<E>(pk64);
 #pragma unroll
         for (int j = 0; j < E; ++j) {
             const uint32_t i = lane * E + j;
