@@ -587,7 +587,27 @@ __device__ __forceinline__ uint32_t wave_chunk(const R (&r)[kWRPT], uint32_t n, 
     uint32_t keptm = 0, ecnt[kWPPL];
 #pragma unroll
     for (int j = 0; j < kWPPL && j < (int)jn; ++j) pkv[j] = pkey_d[lane + 64u * j];
-    if constexpr (!per_pid) {
+    if constexpr (ItemTraits<Item>::preagg) {
+        // ---- pre-aggregate (no bounds): every pair is kept with all of its
+        // records, so phases C-F reduce to the pair counts and one value
+        // sum per record (no thresholds, states or samples to compute)
+#pragma unroll
+        for (int j = 0; j < kWPPL && j < (int)jn; ++j) {
+            if (lane + 64u * j < npair) keptm |= 1u << j;
+            ecnt[j] = pcnt[lane + 64u * j];
+        }
+        if (need_v) {
+            double v[kWRPT];
+#pragma unroll
+            for (int k = 0; k < kWRPT && k < (int)kn; ++k)
+                v[k] = ((insm >> k) & 1u) ? rec_value<R>(cur[k], bp.value, f) : 0.0;
+#pragma unroll
+            for (int k = 0; k < kWRPT && k < (int)kn; ++k)
+                if ((insm >> k) & 1u) atomicAdd(&acc_sum[dn[k]], v[k]);
+            wave_sync();
+        }
+        mark(bp, 7, clk);
+    } else if constexpr (!per_pid) {
         // ---- C1: candidates (priority below the pid's threshold) append
         // their pair key to the pid's region
         uint32_t sb[kWPPL], m[kWPPL];
