@@ -354,15 +354,15 @@ __device__ __forceinline__ int sort_chunk(uint32_t nc, char *smem, const BoundPa
     bool sorted_packed = false;
     if constexpr (!kWPk && !kLex && E <= 4 && DPG_SORT_PACKED) {
         // keys alone (2 VALU per in-lane compare-exchange, see
-        // bitonic_sort_keys_f64): tag bits 01 | pid slot (7 bits) | top 45 -
-        // pkbits bits of the pair priority | pk | candidate position (9
-        // bits); the full keys and record indices are read back by position.
+        // bitonic_sort_keys_f64): tag bits 01 | pid slot (7 bits) | top
+        // min(32, 45 - pkbits) bits of the pair priority | pk | candidate
+        // position (9 bits); the full keys and record indices are read back by position.
         // Two pairs of one pid whose priorities agree in the kept bits (~24^2
         // / 2^26 per pid at pkbits 20) may come out in pk order instead of
         // priority order: the full keys are then not ascending and the chunk
         // is sorted again with key and payload.
         const uint32_t pkb = f.pkbits;
-        const uint32_t ppb = 45u - pkb;
+        const uint32_t ppb = min(32u, 45u - pkb);  // all 32 bits when pk is narrow
         const uint64_t pkm = (1ull << pkb) - 1ull;
         uint64_t pk64[E];
 #pragma unroll
