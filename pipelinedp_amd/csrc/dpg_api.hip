@@ -962,7 +962,10 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     // the items are partitioned by partition-key range: one level up to 1024
     // ranges, else two (pk >> (rbits + b2), then (pk >> rbits) mod 2^b2) --
     // the final segment index is the range id either way
-    constexpr uint32_t kRB = kPA ? 11u : (uint32_t)kRangeBits;
+#ifndef DPG_PA_RB
+#define DPG_PA_RB 11  // pre-aggregate: low partition-key bits sorted by the last (pairs) level
+#endif
+    constexpr uint32_t kRB = kPA ? (uint32_t)DPG_PA_RB : (uint32_t)kRangeBits;
     const int64_t nranges = (P + (1ll << kRB) - 1) >> kRB;
     int64_t *baseR = nullptr;
     uint32_t *totR = nullptr;
