@@ -199,15 +199,16 @@ __global__ __launch_bounds__(256) void k_select_noise(const int64_t *rows, const
         const int kind = z.kind;
         if (z.family == DPG_FAMILY_VARIANCE) {
             // dp_computations.py:307-366
-            double dc = add_noise(kind, cnt, z.scale[DPG_SLOT_COUNT], G[DPG_SLOT_COUNT], seed, gk, DPG_SLOT_COUNT);
+            double dc = add_noise(kind, cnt, z.scale[DPG_SLOT_COUNT], G[DPG_SLOT_COUNT], seed, gk,
+                                  DPG_SLOT_COUNT);
             double den = dc > 1.0 ? dc : 1.0;
             double mean = z.mean_const ? z.mean_const_value
                                        : add_noise(kind, nsum ? nsum[k] : 0.0,
                                                    z.scale[DPG_SLOT_SUM], G[DPG_SLOT_SUM], seed, gk,
                                                    DPG_SLOT_SUM) / den;
             double msq = z.msq_const ? z.msq_const_value
-                                     : add_noise(kind, nsq ? nsq[k] : 0.0, z.scale[DPG_SLOT_NSQ], G[DPG_SLOT_NSQ],
-                                                 seed, gk, DPG_SLOT_NSQ) / den;
+                                     : add_noise(kind, nsq ? nsq[k] : 0.0, z.scale[DPG_SLOT_NSQ],
+                                                 G[DPG_SLOT_NSQ], seed, gk, DPG_SLOT_NSQ) / den;
             double var = msq - mean * mean;
             if (!z.mean_const) mean += z.mid;
             V[DPG_V_VARIANCE] = var;
@@ -216,9 +217,10 @@ __global__ __launch_bounds__(256) void k_select_noise(const int64_t *rows, const
             V[DPG_V_MEAN] = mean;
         } else if (z.family == DPG_FAMILY_MEAN) {
             // dp_computations.py:563-569
-            double dc = add_noise(kind, cnt, z.scale[DPG_SLOT_COUNT], G[DPG_SLOT_COUNT], seed, gk, DPG_SLOT_COUNT);
-            double dn = add_noise(kind, nsum ? nsum[k] : 0.0, z.scale[DPG_SLOT_SUM], G[DPG_SLOT_SUM], seed, gk,
-                                  DPG_SLOT_SUM);
+            double dc = add_noise(kind, cnt, z.scale[DPG_SLOT_COUNT], G[DPG_SLOT_COUNT], seed, gk,
+                                  DPG_SLOT_COUNT);
+            double dn = add_noise(kind, nsum ? nsum[k] : 0.0, z.scale[DPG_SLOT_SUM], G[DPG_SLOT_SUM],
+                                  seed, gk, DPG_SLOT_SUM);
             double mean = z.mid + dn / (dc > 1.0 ? dc : 1.0);
             V[DPG_V_COUNT] = dc;
             V[DPG_V_SUM] = mean * dc;
@@ -226,14 +228,16 @@ __global__ __launch_bounds__(256) void k_select_noise(const int64_t *rows, const
         } else {
             if (z.slot_mask & (1u << DPG_SLOT_COUNT))
                 V[DPG_V_COUNT] =
-                    add_noise(kind, cnt, z.scale[DPG_SLOT_COUNT], G[DPG_SLOT_COUNT], seed, gk, DPG_SLOT_COUNT);
+                    add_noise(kind, cnt, z.scale[DPG_SLOT_COUNT], G[DPG_SLOT_COUNT], seed, gk,
+                              DPG_SLOT_COUNT);
             if (z.slot_mask & (1u << DPG_SLOT_SUM))
-                V[DPG_V_SUM] = add_noise(kind, sum ? sum[k] : 0.0, z.scale[DPG_SLOT_SUM], G[DPG_SLOT_SUM], seed,
-                                         gk, DPG_SLOT_SUM);
+                V[DPG_V_SUM] = add_noise(kind, sum ? sum[k] : 0.0, z.scale[DPG_SLOT_SUM],
+                                         G[DPG_SLOT_SUM], seed, gk, DPG_SLOT_SUM);
         }
         if (z.slot_mask & (1u << DPG_SLOT_PID))
             V[DPG_V_PRIVACY_ID_COUNT] =
-                add_noise(kind, (double)r, z.scale[DPG_SLOT_PID], G[DPG_SLOT_PID], seed, gk, DPG_SLOT_PID);
+                add_noise(kind, (double)r, z.scale[DPG_SLOT_PID], G[DPG_SLOT_PID], seed, gk,
+                          DPG_SLOT_PID);
         for (int j = 0; j < z.n_out; ++j) o[j] = V[z.out_src[j]];
     }
 }
