@@ -47,7 +47,10 @@ namespace dpg {
 // mpc + 2 sqrt(mpc) + 2: BoundParams::cand_mul); restarts (a pid short of
 // mpc candidate pairs) cost a second round, candidates past 64 / 128 / 256
 // per chunk a sort twice as wide
-constexpr float kSortCandC = 1.5f;  // same-box A/B, config 2 bound: 2.0 9.03 ms, 1.5 7.49, 1.25 7.47 + more restarts
+// same-box A/Bs of the config-2 bounding stage: 2.0 9.03 ms, 1.5 7.49, 1.25
+// 7.47 (round 3); with the float64 network 1.75 7.38, 1.5 6.83, 1.35 6.70,
+// 1.25 6.81 (round 4, profiles/r4/r4p_cand_mult_ab.txt)
+constexpr float kSortCandC = 1.35f;
 
 constexpr uint32_t kSkPkBits = 24;  // partition-key bits of the sort key
 #ifndef DPG_SORT_PACKED
