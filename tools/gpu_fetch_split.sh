@@ -4,8 +4,11 @@
 # library and with a build whose value reads return 0 (-DDPG_EXP_NO_GATHER=1,
 # pipelinedp_amd/lib/libdpg_nogather.so: same records, same kept pairs, no
 # gathers).  Results: gpurun_out/split/hbm_{prod,nogather}.json.
+# Build the variant first, on the CPU: python tools/build_variant.py
+# libdpg_nogather.so -DDPG_EXP_NO_GATHER=1
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
+[ -f $R/pipelinedp_amd/lib/libdpg_nogather.so ] || { echo "libdpg_nogather.so missing (see header)"; exit 1; }
 export TMPDIR=/tmp
 O=$R/gpurun_out/split
 mkdir -p $O
