@@ -21,10 +21,13 @@ Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--records R]
 options: --dist-backend nccl (RCCL, default; one GPU per rank) or gloo (host-
 staged collectives; ranks may share a GPU: rank r uses GPU r mod #GPUs, which
 is how a one-GPU box rehearses the N-rank path), --exchange auto |
-reduce_scatter | all_to_all (distributed.exchange_partials), --check-single
-(after timing, rank 0 re-runs the union of every rank's records as ONE rank
-with the release nonce of the N-rank run and reports whether the kept
-partition sets and the exact columns agree).
+reduce_scatter | all_to_all (distributed.exchange_partials).  After timing,
+every multi-rank run checks itself (distributed.check_single; --no-check-single
+skips it): each rank keeps the first --check-records of its records (default
+min(records, 1e8, 4e8 / N)), the N ranks release them with a fixed nonce, the
+prefixes are gathered to rank 0, which releases their union as ONE rank with
+the same nonce, and the line reports whether the kept partition sets and the
+exact columns agree (the selected set does not depend on N).
 """
 import argparse
 import hashlib
@@ -44,13 +47,29 @@ METRIC = "records/sec DPEngine.aggregate COUNT+SUM at 1/2/4/8 MI355X; % HBM roof
 HBM_PEAK_GBS = 8000.0
 ALGO_BYTES_PER_RECORD = 24  # pid int64 + pk int64 + value f64
 CPU_SHARE = 16              # host cores of one GPU's share on the GPU box
-# reference LocalBackend (stub PyDP, 1 Python thread), measured in the build
-# container (synthetic 1M-record row) -- context only
-REFERENCE_LOCAL_BACKEND = {"value": 1.13e5, "unit": "records/s", "cores": 1,
-                           "kind": "reference",
-                           "sample": "reference LocalBackend, 1e6 records / 1e4 pids / 1e3 "
-                                     "Zipf partitions, no-noise PyDP stub, build container "
-                                     "(BASELINE.md section 2); not re-run on the GPU box"}
+
+
+def reference_local_backend():
+    """The reference's own CPU path (LocalBackend, stub PyDP, one Python
+    thread), timed in the build container by tools/time_reference_cpu.py on
+    this bench's generator at 1e6 and 1e7 records (profiles/cpu_ref_r05.json;
+    the reference cannot travel to the GPU box) -- context beside the C-port
+    baseline, at the largest size timed."""
+    f = os.path.join(ROOT, "profiles", "cpu_ref_r05.json")
+    try:
+        d = json.load(open(f))
+    except (OSError, ValueError):
+        return None
+    run = max(d["runs"], key=lambda r: r["records"])
+    return {"value": run["records_per_s"], "unit": "records/s", "cores": d["cores"],
+            "kind": "reference",
+            "sample": f"reference LocalBackend DPEngine.aggregate, {run['records']:.0e} records of "
+                      f"this bench's generator ({run['privacy_ids']:.0e} privacy ids, "
+                      f"{run['partitions']:.0e} Zipf partitions), mpc 8 / mcpp 2, no-noise PyDP "
+                      f"stand-in, build container ({d['host']['nproc']} cores, 1 used), "
+                      f"{d['date']}; {os.path.relpath(f, ROOT)}",
+            "runs": [{"records": r["records"], "records_per_s": round(r["records_per_s"])}
+                     for r in d["runs"]]}
 
 
 def zipf_cdf(P: int, s: float, device) -> torch.Tensor:
@@ -217,7 +236,7 @@ def cpu_baseline(args, P):
                       f"generator (one privacy-id range per core); C oracle full path: "
                       f"bounding+merge in {k} processes (slowest {slowest:.1f} s), merge of "
                       f"the shards' partials, selection + noise; {dt:.1f} s wall",
-            "reference_local_backend": REFERENCE_LOCAL_BACKEND}
+            "reference_local_backend": reference_local_backend()}
 
 
 def make_params(args):
@@ -434,7 +453,12 @@ def main():
     ap.add_argument("--exchange", choices=["auto", "reduce_scatter", "all_to_all"],
                     default="auto")
     ap.add_argument("--check-single", action="store_true",
-                    help="multi-rank: compare the kept set with a one-rank run of all records")
+                    help="(default for N > 1; kept for compatibility)")
+    ap.add_argument("--no-check-single", action="store_true",
+                    help="multi-rank: skip the one-rank equality check after timing")
+    ap.add_argument("--check-records", type=int, default=None,
+                    help="records per rank in the one-rank check (default min(records, 1e8, "
+                         "4e8 / N))")
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(_launch_ranks(args.gpus))
@@ -520,6 +544,16 @@ def main():
         torch.distributed.barrier()
     wall = time.perf_counter() - t0
     dev_ms = ev0.elapsed_time(ev1) / args.steps
+    # untimed: what a caller that does not declare the privacy-id range pays
+    # on top (the device min / max pass over the pid column, stage "pidrange")
+    nohint = pdp.ColumnarData(pid=pid, pk=pk, value=val, n_partitions=P,
+                              record_id_offset=rank * args.records)
+    acc_nh = pdp.NaiveBudgetAccountant(1.0, 1e-6)
+    r_nh = pdp.DPEngine(acc_nh, backend).aggregate(nohint, params, ex, public_partitions=public)
+    acc_nh.compute_budgets()
+    r_nh.materialize(gather=False)
+    pidrange_ms = backend.ctx.stage_times().get("pidrange")
+    del r_nh, nohint
     per_rank = [[wall, dev_ms]]
     if group is not None:
         cdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
@@ -581,7 +615,11 @@ def main():
                    "noise": "gaussian" if c4 else "laplace",
                    "epsilon": 1.0, "delta": 1e-6,
                    "selection": "public" if public is not None else "truncated_geometric",
-                   "parallelism": f"pid-sharded x{world}"},
+                   "parallelism": f"pid-sharded x{world}",
+                   # caller metadata, like n_partitions: the timed calls skip
+                   # the device min / max of the pid column (its cost, from an
+                   # untimed call without the hint: kernels["pidrange_untimed"])
+                   "privacy_id_range_supplied": True},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "traffic": (tj["bytes_per_step"] if tj else None),
@@ -595,6 +633,13 @@ def main():
         "kept_partitions": kept, "kept_pairs": kept_pairs, "kept_records": kept_recs,
         "lib_sha256": _lib_sha(),
     }
+    if pidrange_ms is not None:
+        b = stage_design_bytes("pidrange", args.records, rec_bytes, item_bytes, 0, 0, P, n_accum)
+        kernels["pidrange_untimed"] = {
+            "ms": round(pidrange_ms, 4), "design_bytes": b,
+            "achieved_gbs": round(b / (pidrange_ms * 1e-3) / 1e9, 1),
+            "note": "one call WITHOUT privacy_id_range (not in the timed steps): the extra "
+                    "device min/max pass a caller that does not declare the range pays"}
     if tj:
         line["roofline"]["traffic_by_kernel"] = tj.get("kernels")
     if cpu is not None:
@@ -608,23 +653,35 @@ def main():
             "exchange": res.last_exchange,
             "rank_ms_per_step": [r[0] / args.steps * 1e3 for r in per_rank],
             "rank_device_ms": [r[1] for r in per_rank]}
-        if args.check_single:
+        if not args.no_check_single:
             line["distributed"]["check_single"] = check_single(
-                args, cols, params, public, world, rank, dev, group)
+                args, (pid, pk, val), params, public, world, rank, dev, group)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if group is not None:
         torch.distributed.destroy_process_group()
 
 
-def check_single(args, cols, params, public, world, rank, dev, group):
-    """One N-rank release with a fixed nonce against ONE rank over the union
-    of every rank's records (rank 0 regenerates the other ranks' shards from
-    their seeds): the kept partition sets and the integer columns (count,
-    privacy id count) must be equal, sums equal to 1e-9."""
+def check_single(args, data, params, public, world, rank, dev, group):
+    """The N-rank path against ONE rank, on a bounded prefix of every rank's
+    records (the selected set must not depend on the number of
+    GPUs).  Each rank keeps its first m records (global record ids rank * m
+    + i, so that the concatenation in rank order carries the same ids); the
+    N ranks release them with a fixed nonce; the prefixes are gathered to
+    rank 0 (RCCL point-to-point, or through the host for gloo), which
+    releases their union as one rank with the same nonce.  Kept partition
+    sets and the integer columns (count, privacy id count) must be equal,
+    the other columns equal to 1e-9 relative."""
     import pipelinedp_amd as pdp
     nonce = 0x5EED0F2A11
+    m = args.check_records or min(args.records, 100_000_000, 400_000_000 // world)
+    m = max(1, min(m, args.records))
+    pid, pk, val = (t[:m] for t in data)
     ex = pdp.DataExtractors("pid", "pk", "value")
+    P = args.partitions
+    cols = pdp.ColumnarData(pid=pid, pk=pk, value=val, n_partitions=P,
+                            privacy_id_range=(rank * args.pids, (rank + 1) * args.pids),
+                            record_id_offset=rank * m)
     backend = pdp.MI355XBackend(device=dev.index, seed=0xD1FF5EED, process_group=group,
                                 exchange=args.exchange)
     acc = pdp.NaiveBudgetAccountant(1.0, 1e-6)
@@ -632,20 +689,33 @@ def check_single(args, cols, params, public, world, rank, dev, group):
     acc.compute_budgets()
     res.nonce = nonce
     out = res.materialize(gather=True)
+    del res, backend
+    # the prefixes to rank 0, in rank order
+    host = args.dist_backend == "gloo"
+    parts = [None] * world
+    if rank == 0:
+        parts[0] = (pid, pk, val)
+        for r in range(1, world):
+            got = []
+            for t in (pid, pk, val):
+                buf = torch.empty(m, dtype=t.dtype, device="cpu" if host else dev)
+                torch.distributed.recv(buf, src=r, group=group)
+                got.append(buf.to(dev))
+            parts[r] = tuple(got)
+    else:
+        for t in (pid, pk, val):
+            torch.distributed.send(t.contiguous().cpu() if host else t.contiguous(), dst=0,
+                                   group=group)
+    torch.distributed.barrier()
     if rank != 0:
         return None
     ids_n = out.partition_ids.cpu().numpy()
     vals_n = out.values.cpu().numpy()
-    P = args.partitions
-    pid_cdf = (pareto_cdf(args.pids, 1.2, args.pid_cap, 4321, dev)
-               if args.workload == "config4" else None)
-    parts = [generate(args.records, args.pids, P, r, 1, dev, pid_cdf) for r in range(world)]
-    pid = torch.cat([p[0] for p in parts])
-    pk = torch.cat([p[1] for p in parts])
-    val = torch.cat([p[2] for p in parts])
-    del parts
-    one = pdp.ColumnarData(pid=pid, pk=pk, value=val, n_partitions=P,
+    one = pdp.ColumnarData(pid=torch.cat([p[0] for p in parts]),
+                           pk=torch.cat([p[1] for p in parts]),
+                           value=torch.cat([p[2] for p in parts]), n_partitions=P,
                            privacy_id_range=(0, world * args.pids), record_id_offset=0)
+    del parts
     acc1 = pdp.NaiveBudgetAccountant(1.0, 1e-6)
     res1 = pdp.DPEngine(acc1, pdp.MI355XBackend(device=dev.index, seed=0xD1FF5EED)).aggregate(
         one, params, ex, public_partitions=public)
@@ -662,9 +732,10 @@ def check_single(args, cols, params, public, world, rank, dev, group):
         ints = [j for j, f in enumerate(fields) if f in ("count", "privacy_id_count")]
         exact_cols = bool(np.array_equal(vals_n[o][:, ints], vals_1[o1][:, ints]))
         close_cols = bool(np.allclose(vals_n[o], vals_1[o1], rtol=1e-9, atol=1e-6))
-    return {"records": int(pid.numel()), "kept_n_rank": int(len(ids_n)),
-            "kept_one_rank": int(len(ids_1)), "same_kept_set": same_set,
-            "integer_columns_equal": exact_cols, "all_columns_close": close_cols}
+    return {"records": int(one.pid.numel()), "records_per_rank": int(m),
+            "kept_n_rank": int(len(ids_n)), "kept_one_rank": int(len(ids_1)),
+            "same_kept_set": same_set, "integer_columns_equal": exact_cols,
+            "all_columns_close": close_cols}
 
 
 if __name__ == "__main__":

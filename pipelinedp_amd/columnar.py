@@ -235,8 +235,12 @@ def encode(col, extractors, device: torch.device, need_values: bool,
     public_ids = None
     # rows whose partition keys are numpy scalars keep those objects as the
     # key table: results and the utility analysis' partition sampler then see
-    # the user's own keys (repr np.int64(5), as the reference's rows print)
-    np_row_keys = isinstance(pk, list) and any(isinstance(k, np.generic) for k in pk)
+    # the user's own keys (repr np.int64(5), as the reference's rows print).
+    # Only without an n_partitions hint: with one, the keys are the caller's
+    # dense ids, and the public bitmap above (pub_range / pub_dense) was
+    # built over those ids, so they must not be re-encoded
+    np_row_keys = (hint is None and isinstance(pk, list)
+                   and any(isinstance(k, np.generic) for k in pk))
     if _integer_like(pk) and not np_row_keys:
         pk_t = _to_tensor(pk, device).to(torch.int64)
         if hint is not None:

@@ -103,6 +103,10 @@ struct dpg_ctx {
     // runs (the team level-2 decision, see pipeline())
     uint32_t *pin_tot = nullptr;
     hipEvent_t tot_ev = nullptr;
+    // a team level-2 barrier timed out once on this context (workgroups not
+    // co-resident: other work shares the GPU): later calls take the
+    // histogram level 2 directly instead of paying the timeout again
+    bool team_timed_out = false;
 };
 
 namespace {
@@ -1242,7 +1246,7 @@ int pipeline(dpg_ctx *ctx, hipStream_t s, const int64_t *pid, const int64_t *pk,
     // registers.  DPG_TEAM_L2=0: the grouped histogram path.
     const uint32_t team_T = (uint32_t)ctx->n_cu / 8;
     bool team = sizeof(R) == 8 && pl.b2 >= 6 && pl.b2 <= kMaxB1 && ctx->n_cu % 8 == 0 && team_T > 0 && l1_grp &&
-                env_int("DPG_TEAM_L2", 1) != 0;
+                env_int("DPG_TEAM_L2", 1) != 0 && !ctx->team_timed_out;
     if constexpr (sizeof(R) != 8) team = false;
     if constexpr (sizeof(R) == 8) if (team) {
         int occ = 0;
@@ -1402,7 +1406,11 @@ int pipeline(dpg_ctx *ctx, hipStream_t s, const int64_t *pid, const int64_t *pk,
     if (r == kRedoLevel2) {
         // a team barrier timed out (workgroups not co-resident): level 2 again
         // with the histogram path, the chunk counters reset
-        std::fprintf(stderr, "[dpg] team level 2 timed out; redone with the histogram path\n");
+        std::fprintf(stderr, "[dpg] team level 2 timed out; redone with the histogram path "
+                             "(and on this context from now on)\n");
+        ctx->team_timed_out = true;
+        // a stage of its own, so that stage times (bench lines) show the redo
+        stage(ctx, s, "partition2:team_redo");
         HIP_TRY(hipMemsetAsync(&ctl->err, 0, 4, s));
         HIP_TRY(hipMemsetAsync(&ctl->n_chunks, 0,
                                offsetof(Control, pid_lo) - offsetof(Control, n_chunks), s));

@@ -220,7 +220,7 @@ class DeviceAggregation:
                 ctx.export_error(err.data_ptr(), sptr)
                 tensors, (pk_offset, pk_stride, local_P), self.last_exchange, flags = \
                     distributed.exchange_partials(tensors, P, backend.process_group,
-                                                  backend.exchange, nnz_bound, err)
+                                                  backend.exchange, nnz_bound, err, ctx, sptr)
                 # any rank's bounding error fails this rank's compaction
                 flags = flags.to(dev).contiguous()
                 ctx.import_error(flags.data_ptr(), flags.numel(), sptr)

@@ -111,12 +111,22 @@ def _unpack_column(col: torch.Tensor, like: torch.Tensor) -> torch.Tensor:
 
 
 def reduce_scatter_partials(tensors: Dict[str, Optional[torch.Tensor]], P: int, group,
-                            err: Optional[torch.Tensor] = None):
+                            err: Optional[torch.Tensor] = None, ctx=None, stream=None):
     """Sums the dense partials over ranks; returns this rank's partitions
     of every array, (lo, stride, n) and the summed error flags (a [1]
     float64 tensor on the partials' device), with one collective for all
     of them.  Layout [rank][array][S] + one error slot per rank block --
-    the C ABI's dpg_pack_partials layout."""
+    the C ABI's dpg_pack_partials layout.
+
+    Device partials with the library context `ctx` (the product path): ONE
+    pack kernel (dpg_pack_partials: every array interleaved into its rank
+    blocks, int64 -> float64, zero past P, the context's error flag in each
+    block's last slot) and ONE unpack kernel (dpg_unpack_partials: this
+    rank's block back into int64 / float64 slices, a nonzero error sum
+    latched for dpg_compact_kept), stream-ordered on `stream` (torch's
+    current stream, which the collective waits on) -- one pass over the
+    partials each way.  Host partials (the gloo CPU tests, no context): the
+    same layout built with torch ops."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     S = (P + world - 1) // world
@@ -124,10 +134,17 @@ def reduce_scatter_partials(tensors: Dict[str, Optional[torch.Tensor]], P: int, 
     names = _names(tensors)
     A = len(names)
     dev = tensors[names[0]].device
+    fused = ctx is not None and dev.type == "cuda"
     pack = torch.empty((world, A * S + 1), dtype=torch.float64, device=dev)
-    for j, k in enumerate(names):
-        pack[:, j * S:(j + 1) * S] = _interleaved(tensors[k], P, world, S)
-    pack[:, A * S] = err.to(dev).reshape(()) if err is not None else 0.0
+    if fused:
+        from pipelinedp_amd import _native
+        full = _native.Partials(P, *(tensors[k].data_ptr() if tensors.get(k) is not None else None
+                                     for k in _PACK_ORDER))
+        ctx.pack_partials(full, world, pack.data_ptr(), stream)
+    else:
+        for j, k in enumerate(names):
+            pack[:, j * S:(j + 1) * S] = _interleaved(tensors[k], P, world, S)
+        pack[:, A * S] = err.to(dev).reshape(()) if err is not None else 0.0
     if _is_nccl(group):
         part = torch.empty(A * S + 1, dtype=torch.float64, device=dev)
         dist.reduce_scatter_tensor(part, pack.view(-1), op=dist.ReduceOp.SUM, group=group)
@@ -135,9 +152,21 @@ def reduce_scatter_partials(tensors: Dict[str, Optional[torch.Tensor]], P: int, 
         host = pack.cpu()
         dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
         part = host[rank].to(dev)
+    del pack
     out: Dict[str, Optional[torch.Tensor]] = {k: None for k in _PACK_ORDER}
-    for j, k in enumerate(names):
-        out[k] = _unpack_column(part[j * S:j * S + n_local], tensors[k])
+    if fused:
+        from pipelinedp_amd import _native
+        for k in names:
+            out[k] = torch.empty(max(n_local, 1), dtype=tensors[k].dtype, device=dev)
+        sl = _native.Partials(n_local, *(out[k].data_ptr() if out.get(k) is not None else None
+                                         for k in _PACK_ORDER))
+        lo_k, n_k = ctx.unpack_partials(part.data_ptr(), P, world, rank, sl, stream)
+        assert (lo_k, n_k) == (lo, n_local), (lo_k, n_k, lo, n_local)
+        for k in names:
+            out[k] = out[k][:n_local]
+    else:
+        for j, k in enumerate(names):
+            out[k] = _unpack_column(part[j * S:j * S + n_local], tensors[k])
     return out, (lo, stride, n_local), part[A * S:A * S + 1]
 
 
@@ -179,7 +208,13 @@ def all_to_all_partials(tensors: Dict[str, Optional[torch.Tensor]], P: int, grou
     rank (pks are unique within one source, so every add is conflict-free
     and the merge is deterministic).  Same result as
     reduce_scatter_partials.  A block with more occupied partitions than cap
-    (impossible when nnz_bound bounds the occupancy) raises the error flag."""
+    (impossible when nnz_bound bounds the occupancy) raises the error flag.
+
+    The send side works on the occupied partitions only: at most K =
+    min(P, nnz_bound) of them, taken by one fixed-size nonzero (no host
+    sync), ordered by owner with a stable sort, so its temporaries are
+    K-sized (the sparse exchange is chosen exactly when K is far below P
+    / R: ADVICE r4)."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     S = (P + world - 1) // world
@@ -188,20 +223,28 @@ def all_to_all_partials(tensors: Dict[str, Optional[torch.Tensor]], P: int, grou
     names = _names(tensors)
     A = len(names)
     dev = tensors[names[0]].device
-    occ = _interleaved(tensors["rows"], P, world, S) > 0          # [world, S]
-    pos = occ.to(torch.int64).cumsum(1) - 1
-    fits = occ & (pos < cap)
-    over = (occ & ~fits).any().to(torch.float64)
+    K = max(1, min(P, int(nnz_bound)))
+    occ = tensors["rows"] > 0
+    n_occ = occ.sum()
+    idx = torch.nonzero_static(occ, size=K, fill_value=P).view(-1)   # ascending, pad P
+    valid = idx < P
+    own = torch.where(valid, idx % world, torch.full_like(idx, world))
+    order = torch.argsort(own, stable=True)                          # by owner, pk ascending
+    idx, own, valid = idx[order], own[order], valid[order]
+    cnt = torch.bincount(own, minlength=world + 1)
+    start = torch.cumsum(cnt, 0) - cnt
+    pos = torch.arange(K, device=dev) - start[own]
+    fits = valid & (pos < cap)
+    over = ((n_occ > K) | (valid & ~fits).any()).to(torch.float64)
     blk = cap + 1                                                  # header row + cap rows
     sink = world * blk                                             # rows past the cap, padding
-    dst = torch.where(fits, torch.arange(world, device=dev).view(-1, 1) * blk + 1 + pos,
-                      torch.full_like(pos, sink))
-    grid = (torch.arange(S, device=dev).view(1, -1) * world +
-            torch.arange(world, device=dev).view(-1, 1)).to(torch.float64)
-    rows = torch.stack([grid] + [_interleaved(tensors[k], P, world, S) for k in names], -1)
+    dst = torch.where(fits, own * blk + 1 + pos, torch.full_like(pos, sink))
+    safe = torch.where(valid, idx, torch.zeros_like(idx))
+    rows = torch.stack([idx.to(torch.float64)] +
+                       [tensors[k][safe].to(torch.float64) for k in names], -1)
     send = torch.zeros((sink + 1, 1 + A), dtype=torch.float64, device=dev)
     send[:, 0] = -1.0
-    send.index_copy_(0, dst.reshape(-1), rows.reshape(-1, 1 + A))
+    send.index_copy_(0, dst, rows)
     hdr = torch.arange(world, device=dev) * blk
     send[hdr, 0] = -2.0
     send[hdr, 1] = (err.to(dev).reshape(()) if err is not None else 0.0) + over
@@ -231,12 +274,13 @@ def all_to_all_partials(tensors: Dict[str, Optional[torch.Tensor]], P: int, grou
 
 def exchange_partials(tensors: Dict[str, Optional[torch.Tensor]], P: int, group,
                       mode: str = "auto", nnz_bound: Optional[int] = None,
-                      err: Optional[torch.Tensor] = None):
+                      err: Optional[torch.Tensor] = None, ctx=None, stream=None):
     """Merges the partials of every rank into this rank's partitions with
     the exchange `choose_exchange` picks.  nnz_bound must be the same on
-    every rank (release_header); None = P.  Returns (tensors, (lo, stride,
-    n), info, error flags) where info names the exchange and its per-rank
-    send bytes."""
+    every rank (release_header); None = P.  ctx / stream: the library
+    context and its stream, for the fused pack / unpack kernels of the
+    dense exchange.  Returns (tensors, (lo, stride, n), info, error flags)
+    where info names the exchange and its per-rank send bytes."""
     names = _names(tensors)
     world = dist.get_world_size(group)
     bound = P if nnz_bound is None else int(nnz_bound)
@@ -244,7 +288,7 @@ def exchange_partials(tensors: Dict[str, Optional[torch.Tensor]], P: int, group,
     if chosen == "all_to_all":
         out, own, flags = all_to_all_partials(tensors, P, group, bound, err)
     else:
-        out, own, flags = reduce_scatter_partials(tensors, P, group, err)
+        out, own, flags = reduce_scatter_partials(tensors, P, group, err, ctx, stream)
     info = {"mode": chosen, "backend": dist.get_backend(group), "world_size": world,
             "nnz_bound": bound,
             "send_bytes": exchange_bytes(P, bound, len(names), world)[chosen]}

@@ -94,8 +94,12 @@ def host_preaggregated_pairs(col, extractors, public_partitions, dev) -> PairSet
         arr["sum"][:n] = pre_a[:, 1]
         arr["np"][:n] = pre_a[:, 2]
         if pre_a.shape[1] > 3:
-            # the word's top bit is the leader flag (unused for these rows)
-            arr["ncl"][:n] = np.minimum(pre_a[:, 3], NC_MASK)
+            # the word's top bit is the leader flag (unused for these rows):
+            # n_contributions must fit the remaining 31 bits, as in
+            # dpg_preaggregate (a clamp would bin L0 / L1 silently wrong)
+            if pre_a[:, 3].max() > NC_MASK or pre_a[:, 3].min() < 0:
+                raise ValueError(f"n_contributions must lie in [0, {NC_MASK}] (31 bits)")
+            arr["ncl"][:n] = pre_a[:, 3]
     starts = np.searchsorted(ids[order], np.arange(P + 1)).astype(np.int64)
     pairs = torch.from_numpy(arr.view(np.float64).reshape(-1, PAIR_WORDS).copy()).to(dev)
     return PairSet(pairs, torch.from_numpy(starts).to(dev), P, n, table, pub_mask)

@@ -86,3 +86,23 @@ def test_integer_data_keys_with_non_integer_public_partitions():
     bits = np.unpackbits(enc.public_mask.numpy(), bitorder="little")[:enc.n_partitions]
     assert sorted(str(keys[i]) for i in np.nonzero(bits)[0]) == ["5", "7", "x"]
     assert enc.public_count == 3
+
+
+def test_numpy_scalar_key_list_with_declared_partitions_stays_dense():
+    # a columnar pk list of numpy scalars with n_partitions and
+    # public partitions must keep the caller's dense ids (the public bitmap
+    # is built over them), not be re-encoded through a key table
+    pk = [np.int64(k) for k in (2, 40, 7, 2)]
+    ex = pdp.DataExtractors("pid", "pk", "value")
+    for pub in (range(0, 45), np.array([2, 7, 44]), [2, 7, 44]):
+        col = {"pid": np.array([1, 2, 3, 4]), "pk": pk, "value": np.ones(4), "n_partitions": 45}
+        enc = columnar.encode(col, ex, CPU, True, public_partitions=pub)
+        assert enc.key_table is None and enc.n_partitions == 45 and enc.partitions_declared
+        assert enc.pk.tolist() == [2, 40, 7, 2]
+        bits = np.unpackbits(enc.public_mask.numpy(), bitorder="little")[:45]
+        want = list(pub) if isinstance(pub, range) else [2, 7, 44]
+        assert np.nonzero(bits)[0].tolist() == want
+    # without the hint, numpy-scalar row keys still keep their own objects
+    enc = columnar.encode([(1, np.int64(3), 1.0), (2, np.int64(9), 2.0)], EX, CPU, True)
+    assert enc.key_table is not None
+    assert [type(k) for k in enc.key_table] == [np.int64, np.int64]

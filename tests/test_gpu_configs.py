@@ -127,6 +127,25 @@ def test_config2_level2_paths_match_oracle(built, config2_data, monkeypatch, mod
     assert ("partition1:hist" in stages) == (mode != "pieces")
     assert ("partition2:team" in stages) == (mode != "grouped")
     assert ("partition2:hist" in stages) == (mode in ("grouped", "team_abort"))
+    assert ("partition2:team_redo" in stages) == (mode == "team_abort")
+    if mode == "team_abort":
+        # the timeout is sticky on the context: the next release on the same
+        # backend takes the histogram level 2 directly, and
+        # still matches the oracle
+        monkeypatch.delenv("DPG_DEBUG_TEAM_ABORT")
+        acc = pdp.NaiveBudgetAccountant(1.0, 1e-6)
+        cols = pdp.ColumnarData(pid=torch.from_numpy(pid).cuda(), pk=torch.from_numpy(pk).cuda(),
+                                value=torch.from_numpy(val).cuda(), n_partitions=P2)
+        res2 = pdp.DPEngine(acc, res.backend).aggregate(
+            cols, _c2_params(8, 2), pdp.DataExtractors("pid", "pk", "value"))
+        acc.compute_budgets()
+        res2.noise_enabled = False
+        res2.nonce = 1234
+        res2.materialize()
+        got2 = {k: v.cpu().numpy() for k, v in res2.last_partials.items() if v is not None}
+        _assert_partials(got2, ref)
+        stages2 = res.backend.ctx.stage_times()
+        assert "partition2:team" not in stages2 and "partition2:hist" in stages2
 
 
 def test_config2_pieces_range_error(built, config2_data, monkeypatch):

@@ -84,3 +84,18 @@ def test_range_bitmap_rejects_out_of_range():
     from pipelinedp_amd import columnar
     with pytest.raises(ValueError, match="outside"):
         columnar._range_bitmap(0, 11, 10, torch.device("cpu"))
+
+
+def test_preaggregated_rows_reject_n_contributions_past_31_bits():
+    # the pair word shares its top bit with the leader flag; a
+    # larger n_contributions must raise, not be clamped into wrong L0/L1 bins
+    from pipelinedp_amd import pre_aggregation as pa
+    import pipelinedp_amd as pdp
+    ex = pdp.PreAggregateExtractors(partition_extractor=lambda r: r[0],
+                                    preaggregate_extractor=lambda r: r[1])
+    ok = pa.host_preaggregated_pairs([("a", (1, 2.0, 1, pa.NC_MASK))], ex, None,
+                                     torch.device("cpu"))
+    assert int(pa.to_numpy(ok)["ncl"][0]) == pa.NC_MASK
+    for bad in (pa.NC_MASK + 1, 2**40, -1):
+        with pytest.raises(ValueError, match="n_contributions"):
+            pa.host_preaggregated_pairs([("a", (1, 2.0, 1, bad))], ex, None, torch.device("cpu"))
