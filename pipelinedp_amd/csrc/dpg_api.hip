@@ -373,9 +373,30 @@ int run_level_grouped(dpg_ctx *ctx, hipStream_t s, const Src &src, uint32_t S,
                               (int)lds);
     stage(ctx, s, (t + ":scatter").c_str());
     const uint32_t gs = std::min<uint32_t>(max_subs, (uint32_t)ctx->n_cu);  // one per CU
+#ifdef DPG_PHASE_TIMING
+    const bool ptime = std::getenv("DPG_PHASE_TIMING") != nullptr;
+    if (ptime) {
+        unsigned long long z[8] = {};
+        HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_scat_cyc), z, sizeof(z), 0,
+                                       hipMemcpyHostToDevice, s));
+    }
+#endif
     kern<<<gs, kScatThreads, lds, s>>>(src, tiles, ntiles_dev, F, bits, nullptr, base, out, xq,
                                        nullptr, nullptr, nullptr, 1u, hist, 0u, 0u, nullptr);
     LAUNCH_CHECK();
+#ifdef DPG_PHASE_TIMING
+    if (ptime) {
+        unsigned long long h[8];
+        HIP_TRY(hipMemcpyFromSymbolAsync(h, HIP_SYMBOL(g_scat_cyc), sizeof(h), 0,
+                                         hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        static const char *nm[5] = {"rank", "scan", "stage", "write", "tile"};
+        std::fprintf(stderr, "[dpg] %s scatter phases (wave-0 cycles per workgroup, %u WGs, "
+                             "%.1f sub-tiles each):", tag, gs, (double)h[5] / gs);
+        for (int k = 0; k < 5; ++k) std::fprintf(stderr, " %s %.0f", nm[k], (double)h[k] / gs);
+        std::fprintf(stderr, "\n");
+    }
+#endif
     *base_out = base;
     *tot_out = tot;
     return DPG_OK;

@@ -255,6 +255,25 @@ __host__ __device__ __forceinline__ uint32_t pid_hash(uint64_t seed, uint64_t pi
     const uint32_t h = fmix32((uint32_t)seed ^ DPG_TAG_PAIR ^ (uint32_t)pid);
     return fmix32(h ^ (uint32_t)(pid >> 32) ^ (uint32_t)(seed >> 32));
 }
+#ifndef DPG_PRIO_PHILOX
+#define DPG_PRIO_PHILOX 0
+#endif
+#if DPG_PRIO_PHILOX
+// Cost experiment only: the same
+// priorities drawn from Philox4x32-10 keyed by the per-pid state, as a
+// counter-based RNG would draw them.  Not the shipped sampler: the oracle
+// restates the fmix32 chains below, so parity tests fail against this build.
+__host__ __device__ __forceinline__ uint32_t pair_prio_h(uint32_t hp, uint32_t pk) {
+    uint32_t c[4] = {hp, pk, DPG_TAG_PAIR, 0u};
+    philox4x32_10(c, hp, DPG_TAG_PAIR);
+    return c[0];
+}
+__host__ __device__ __forceinline__ uint64_t rec_prio_h(uint32_t hp, uint32_t pk, uint64_t gidx) {
+    uint32_t c[4] = {pk, (uint32_t)gidx, (uint32_t)(gidx >> 32), DPG_TAG_REC};
+    philox4x32_10(c, hp, DPG_TAG_REC);
+    return ((uint64_t)c[0] << 32) | (uint32_t)gidx;
+}
+#else
 __host__ __device__ __forceinline__ uint32_t pair_prio_h(uint32_t hp, uint32_t pk) {
     return fmix32(hp ^ pk);
 }
@@ -265,6 +284,7 @@ __host__ __device__ __forceinline__ uint64_t rec_prio_h(uint32_t hp, uint32_t pk
     h = fmix32(h ^ (uint32_t)(gidx >> 32));
     return ((uint64_t)h << 32) | (uint32_t)gidx;
 }
+#endif
 __device__ __forceinline__ uint32_t pair_prio(uint64_t seed, uint64_t pid, uint32_t pk) {
     return pair_prio_h(pid_hash(seed, pid), pk);
 }

@@ -643,29 +643,49 @@ __device__ __forceinline__ uint32_t block_scan_digits_t(const uint32_t *cnt, uin
     return total;
 }
 
-// Scatter's per-sub-tile digit scan: dstart[0, F] <- exclusive prefix of
-// cnt (dstart[F] = total), and for every digit cur[d] += cnt[d], cnt[d] = 0
-// (the write-out then addresses cur[d] - dstart[d + 1] + k).  Grouped mode
-// (goff: the group's digit offsets): the sub-tile reserves its run of every
-// digit it holds inside its group by one atomic add, cur[d] += reserved
-// start + cnt[d].  Two barriers: the wave totals' buffer is next written one
-// sub-tile later, behind the caller's own barriers.  Piece mode (kCap): goff
-// are the cursors of fixed-capacity regions; a run that does not fit raises
-// err bit 16 and goes to the dump area at `dump` instead (the host redoes
-// the level with the histogram path).
-template <int T, int DPT, bool kCap = false>
-__device__ __forceinline__ uint32_t scatter_scan_update(uint32_t *cnt, uint32_t *dstart,
-                                                        uint32_t *cur, uint32_t F,
-                                                        uint32_t *sh16, uint32_t *goff = nullptr,
-                                                        uint32_t cap = 0, uint32_t dump = 0,
-                                                        uint32_t *err = nullptr) {
+// Scatter's per-sub-tile digit scan, in two halves around the staging of
+// the sub-tile (k_scatter):
+//
+// scatter_scan_begin: dstart[0, F] <- exclusive prefix of cnt (dstart[F] =
+// total), cnt[d] = 0; grouped / piece mode (goff: the group's digit offsets,
+// or the cursors of the fixed-capacity piece regions) also ISSUES the
+// sub-tile's run reservation of every digit it holds -- one atomic add per
+// digit, unconditional (a count of 0 adds 0) so that both of a thread's
+// atomics are in flight together -- and keeps the returned offsets in
+// registers (ScanRes).  Two barriers: the wave totals' buffer is next
+// written one sub-tile later, behind the caller's own barriers.
+//
+// scatter_scan_finish (after the staging, before the barrier that precedes
+// the write-out): cur[d] += reserved start + cnt[d] (grouped), += cnt[d]
+// (plain); the write-out then addresses cur[d] - dstart[d + 1] + k.  Piece
+// mode (kCap): a run that does not fit its region raises err bit 16 and
+// goes to the dump area at `dump` instead (the host redoes the level with
+// the histogram path).
+//
+// Round 3/4 form: the reservation atomics sat inside the scan, each behind
+// its own branch whose s_waitcnt vmcnt(0) waited for the returned offset
+// before the next was issued -- two serialised atomic round trips per
+// sub-tile on the critical path of the level-1 scatter.
+template <int DPT>
+struct ScanRes {
+    uint32_t c[DPT], o[DPT], e[DPT];
+};
+template <int T, int DPT>
+__device__ __forceinline__ uint32_t scatter_scan_begin(uint32_t *cnt, uint32_t *dstart, uint32_t F,
+                                                       uint32_t *sh16, uint32_t *goff,
+                                                       ScanRes<DPT> &sr) {
     constexpr int NW = T / 64;
     const uint32_t d0 = DPT * threadIdx.x;
-    uint32_t c[DPT], x = 0;
+    uint32_t x = 0;
 #pragma unroll
     for (int u = 0; u < DPT; ++u) {
-        c[u] = d0 + u < F ? cnt[d0 + u] : 0u;
-        x += c[u];
+        sr.c[u] = d0 + u < F ? cnt[d0 + u] : 0u;
+        x += sr.c[u];
+    }
+    if (goff) {
+#pragma unroll
+        for (int u = 0; u < DPT; ++u)
+            sr.o[u] = atomicAdd(&goff[min(d0 + u, F - 1)], sr.c[u]);
     }
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     uint32_t wt;
@@ -681,30 +701,41 @@ __device__ __forceinline__ uint32_t scatter_scan_update(uint32_t *cnt, uint32_t 
     }
 #pragma unroll
     for (int u = 0; u < DPT; ++u) {
+        sr.e[u] = e;
         if (d0 + u < F) {
             dstart[d0 + u] = e;
-            if constexpr (kCap) {
-                if (c[u]) {
-                    const uint32_t o = atomicAdd(&goff[d0 + u], c[u]);
-                    if (o + c[u] <= cap) {
-                        cur[d0 + u] += o + c[u];
-                    } else {
-                        cur[d0 + u] = dump + e + c[u];
-                        atomicOr(err, 16u);
-                    }
-                }
-            } else if (goff) {
-                if (c[u]) cur[d0 + u] += atomicAdd(&goff[d0 + u], c[u]) + c[u];
-            } else {
-                cur[d0 + u] += c[u];
-            }
             cnt[d0 + u] = 0;
         }
-        e += c[u];
+        e += sr.c[u];
     }
     if (threadIdx.x == 0) dstart[F] = total;
     __syncthreads();
     return total;
+}
+template <int DPT, bool kCap = false>
+__device__ __forceinline__ void scatter_scan_finish(uint32_t *cur, uint32_t F, const uint32_t *goff,
+                                                    const ScanRes<DPT> &sr, uint32_t cap = 0,
+                                                    uint32_t dump = 0, uint32_t *err = nullptr) {
+    const uint32_t d0 = DPT * threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < DPT; ++u) {
+        if (d0 + u >= F) continue;
+        const uint32_t c = sr.c[u];
+        if constexpr (kCap) {
+            if (c) {
+                if (sr.o[u] + c <= cap) {
+                    cur[d0 + u] += sr.o[u] + c;
+                } else {
+                    cur[d0 + u] = dump + sr.e[u] + c;
+                    atomicOr(err, 16u);
+                }
+            }
+        } else if (goff) {
+            if (c) cur[d0 + u] += sr.o[u] + c;
+        } else {
+            cur[d0 + u] += c;
+        }
+    }
 }
 
 // grid S: base[s][d] = seg_start[s] + exclusive_prefix_d(tot[s][.])  (F <= 4096)
@@ -787,6 +818,28 @@ constexpr size_t scatter_lds() {
            (Src::kDigitFromRec ? 0 : a16((size_t)2 * (kScatThreads * IPT + 1))) +
            (size_t)FMAX * 12 + 80;
 }
+
+// Phase clock of k_scatter (timing build only, -DDPG_PHASE_TIMING): wave 0
+// of every workgroup stamps s_memtime at the phase boundaries of each
+// sub-tile and adds its totals to g_scat_cyc at exit: [0] loop top ->
+// ranked (load waits + decode + LDS ranking + barrier), [1] digit scan
+// (+ reservations issued), [2] staging + reservations consumed + barrier,
+// [3] next loads issued + write-out, [4] tile transitions, [5] sub-tiles.
+#ifdef DPG_PHASE_TIMING
+__device__ unsigned long long g_scat_cyc[8];
+#define DPG_SCAT_MARK(k)                                         \
+    do {                                                         \
+        if (threadIdx.x == 0) {                                  \
+            const uint64_t now_ = __builtin_amdgcn_s_memtime();  \
+            scyc[k] += now_ - slast;                             \
+            slast = now_;                                        \
+        }                                                        \
+    } while (0)
+#else
+#define DPG_SCAT_MARK(k) \
+    do {                 \
+    } while (0)
+#endif
 
 // kAgg: wave-aggregated ranking (few digits) instead of one LDS atomic per
 // record; a template parameter so that each kernel holds one ranking path
@@ -884,6 +937,10 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
         t = it;
     }
     if (t == kNone) return;
+#ifdef DPG_PHASE_TIMING
+    uint64_t scyc[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t slast = __builtin_amdgcn_s_memtime();
+#endif
     TileDesc td = uniform_tile(tiles, t);
     load_sub(td.begin, (uint32_t)min<int64_t>(SUB, td.end - td.begin));
     for (;;) {
@@ -911,6 +968,7 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
     __syncthreads();
     uint32_t tn = kNone;
     TileDesc tdn = td;
+    DPG_SCAT_MARK(4);
     for (int64_t sb = td.begin; sb < td.end; sb += SUB) {
         const uint32_t lim = (uint32_t)min<int64_t>(SUB, td.end - sb);  // uniform
         Rec rec[IPT];
@@ -947,8 +1005,12 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
         }
         if (xq.q && tid == 0 && sb == td.begin) sh_next = nq;
         __syncthreads();
-        const uint32_t total = scatter_scan_update<kScatThreads, FMAX / kScatThreads, kPc>(
-            cnt, dstart, cur, F, sh16, gof, pcap, pdump, perr);
+        DPG_SCAT_MARK(0);
+        constexpr int kDPT = FMAX / kScatThreads;
+        ScanRes<kDPT> sres;
+        const uint32_t total =
+            scatter_scan_begin<kScatThreads, kDPT>(cnt, dstart, F, sh16, gof, sres);
+        DPG_SCAT_MARK(1);
         {
             uint32_t ds[IPT];
 #pragma unroll
@@ -960,7 +1022,10 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
                 if constexpr (kSD) sdig[pos] = (uint16_t)(dr[j] & 0xFFFu);
             }
         }
+        // the reservations' offsets have returned while the sub-tile was staged
+        scatter_scan_finish<kDPT, kPc>(cur, F, gof, sres, pcap, pdump, perr);
         __syncthreads();
+        DPG_SCAT_MARK(2);
         const int64_t nb = sb + SUB;
         const uint32_t nlim = (uint32_t)max<int64_t>(0, min<int64_t>(SUB, td.end - nb));
         {
@@ -1019,6 +1084,10 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
         }
         // the next sub-tile's first barrier (after its ranking) orders this
         // write-out's LDS reads before the next scan and staging
+        DPG_SCAT_MARK(3);
+#ifdef DPG_PHASE_TIMING
+        if (tid == 0) ++scyc[5];
+#endif
     }
     if (!HasTilePrefetch<Src>::value && xq.q) {
         // XCD-local without the prefetch: dequeued now, loaded unoverlapped
@@ -1040,6 +1109,10 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
     t = tn;
     td = tdn;
     }
+#ifdef DPG_PHASE_TIMING
+    if (tid == 0)
+        for (int k = 0; k < 6; ++k) atomicAdd(&g_scat_cyc[k], (unsigned long long)scyc[k]);
+#endif
 }
 
 }  // namespace dpg

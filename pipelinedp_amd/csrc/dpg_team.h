@@ -31,6 +31,12 @@
 namespace dpg {
 
 constexpr int kTeamIPT = 16;                       // records per thread
+#ifndef DPG_TEAM_PF
+#define DPG_TEAM_PF 0  // experiment: next share loaded during the barrier + write-out
+#endif
+#ifndef DPG_TEAM_WB
+#define DPG_TEAM_WB 4  // staged records per thread per write-out batch
+#endif
 constexpr uint32_t kTeamF = 2048;                  // digits (11 bits)
 constexpr int kTeamSub = kScatThreads * kTeamIPT;  // records per member per bucket
 constexpr uint64_t kTeamTimeout = 50000000ull;     // wall_clock64 ticks (100 MHz): 0.5 s
@@ -64,13 +70,23 @@ __device__ __forceinline__ uint32_t ld_agent(const uint32_t *p) {
 // poll is an sc1 load.  (Agent-scope fences here -- __threadfence in every
 // thread, a release add, an acquire per poll -- wrote back and invalidated
 // the XCD L2 that holds the scattered runs: 20.5 ms instead of ~4 ms.)
+//
+// `between` runs in every thread after the arrival and before the poll: the
+// loads it issues (the next bucket's share) are in flight during the wait
+// instead of behind the arrival's vmcnt(0).
+struct NoOp {
+    __device__ __forceinline__ void operator()() const {}
+};
+template <class F = NoOp>
 __device__ __forceinline__ bool team_barrier(const TeamSync &ts, uint32_t team, uint32_t target,
-                                             uint32_t *sh_ok) {
+                                             uint32_t *sh_ok, const F &between = F{}) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's reservations / zeroing done
     __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t *ctr = ts.arrive + team * kTeamArriveStride;
+    uint32_t *ctr = ts.arrive + team * kTeamArriveStride;
+    if (threadIdx.x == 0)
         __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    between();
+    if (threadIdx.x == 0) {
         const uint64_t t0 = wall_clock64();
         uint32_t ok = 1;
         while (ld_agent(ctr) < target) {
@@ -226,6 +242,26 @@ __global__ __launch_bounds__(kScatThreads) void k_part2_team(SrcAoS<R> src,
         vmask = vm;
     };
     uint32_t k = 0;  // buckets done = team barriers passed
+    // kPF (contiguous buckets): the share of this member's next non-empty
+    // bucket is loaded during the current bucket's team barrier and
+    // write-out (the local staging moves before the barrier, which frees
+    // the record registers); pf_s = the bucket those registers hold
+    constexpr bool kPF = !kPc && DPG_TEAM_PF;
+    auto next_nonempty = [&](uint32_t s) -> uint32_t {
+        for (; s < S; s += 8)
+            if (__builtin_amdgcn_readfirstlane(seg_cnt[s]) != 0) break;
+        return s;
+    };
+    uint32_t pf_s = S;
+    if constexpr (kPF) {
+        pf_s = next_nonempty(team);
+        if (pf_s < S) {
+            int64_t st;
+            uint32_t n, b0, lim;
+            share(pf_s, st, n, b0, lim);
+            load(st + b0, lim);
+        }
+    }
     for (uint32_t s = team; s < S; s += 8) {
         int64_t st;
         uint32_t n, b0, lim;
@@ -243,7 +279,7 @@ __global__ __launch_bounds__(kScatThreads) void k_part2_team(SrcAoS<R> src,
         if constexpr (kPc) {
             vmask = 0;
             if (lim > 0) load_pieces(s, b0, lim);
-        } else {
+        } else if constexpr (!kPF) {
             load(st + b0, lim);
         }
         uint32_t dr[IPT];
@@ -273,6 +309,14 @@ __global__ __launch_bounds__(kScatThreads) void k_part2_team(SrcAoS<R> src,
                 c[u] = cnt[d0 + u];
                 x += c[u];
             }
+            // the reservations, issued before the scan: unconditional (a
+            // count of 0 adds 0), so that a thread's atomics are in flight
+            // together and overlap the scan, instead of one branch-guarded
+            // round trip after another; the team barrier's vmcnt(0) waits
+            // for them
+            uint32_t o[DPT];
+#pragma unroll
+            for (int u = 0; u < DPT; ++u) o[u] = atomicAdd(&tt[d0 + u], c[u]);
             uint32_t wt;
             uint32_t e = wave_excl_scan(x, wt);
             if (lane == 63) sh16[wv] = wt;
@@ -285,14 +329,34 @@ __global__ __launch_bounds__(kScatThreads) void k_part2_team(SrcAoS<R> src,
 #pragma unroll
             for (int u = 0; u < DPT; ++u) {
                 dstart[d0 + u] = e;
-                cur[d0 + u] = c[u] ? atomicAdd(&tt[d0 + u], c[u]) : 0u;
+                cur[d0 + u] = o[u];
                 cnt[d0 + u] = 0;
                 e += c[u];
             }
             if (tid == 0) dstart[F] = nv;
         }
         ++k;
-        if (!team_barrier(ts, team, T * k, &sh_ok)) return;
+        if constexpr (kPF) {
+            // ---- stage by local digit now (independent of the team totals)
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < IPT; ++j) {
+                const uint32_t pos = dr[j] != ~0u ? dstart[dr[j] & 0xFFFu] + (dr[j] >> 12) : (uint32_t)SUB;
+                stage[pos] = to_words(rec[j]);
+            }
+            pf_s = next_nonempty(s + 8);
+        }
+        auto prefetch = [&]() {
+            if constexpr (kPF) {
+                if (pf_s < S) {
+                    int64_t st2;
+                    uint32_t n2, b2, lim2;
+                    share(pf_s, st2, n2, b2, lim2);
+                    load(st2 + b2, lim2);
+                }
+            }
+        };
+        if (!team_barrier(ts, team, T * k, &sh_ok, prefetch)) return;
         // ---- the bucket's digit starts from the team totals
         {
             const uint32_t d0 = DPT * tid;
@@ -324,15 +388,17 @@ __global__ __launch_bounds__(kScatThreads) void k_part2_team(SrcAoS<R> src,
             }
         }
         // ---- stage by local digit, write every digit's run contiguously
+        if constexpr (!kPF) {
 #pragma unroll
-        for (int j = 0; j < IPT; ++j) {
-            const uint32_t pos = dr[j] != ~0u ? dstart[dr[j] & 0xFFFu] + (dr[j] >> 12) : (uint32_t)SUB;
-            stage[pos] = to_words(rec[j]);
+            for (int j = 0; j < IPT; ++j) {
+                const uint32_t pos = dr[j] != ~0u ? dstart[dr[j] & 0xFFFu] + (dr[j] >> 12) : (uint32_t)SUB;
+                stage[pos] = to_words(rec[j]);
+            }
         }
         __syncthreads();
         // (loading the next bucket's share during the write-out measured
         // slower: 5.2 -> 5.65 ms at config 2, 128 VGPRs with spills)
-        constexpr int WB = 4;
+        constexpr int WB = DPG_TEAM_WB;
         for (uint32_t k0 = 0; k0 < nv; k0 += WB * kScatThreads) {
             W x[WB];
             uint32_t dd[WB], kc[WB];

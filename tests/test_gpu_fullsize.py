@@ -16,6 +16,9 @@ against device group-bys (torch):
 
 This exercises the 32-bit bucket offsets, the level totals and the scratch
 sizes at the size the bench line claims (missing item 3)."""
+import time
+
+import numpy as np
 import pytest
 import torch
 
@@ -28,18 +31,32 @@ N, U, P = 1_000_000_000, 10_000_000, 1_000_000
 SEED = 0xF1115
 
 
+def _log(msg, t0):
+    # progress on stdout (run with -s): these steps take seconds each
+    torch.cuda.synchronize()
+    print(f"[fullsize] {msg}: {time.perf_counter() - t0:.1f} s", flush=True)
+
+
 @pytest.fixture(scope="module")
 def full():
     dev = torch.device("cuda", 0)
+    t0 = time.perf_counter()
     pid, pk, val = bench.generate(N, U, P, 0, 1, dev)
+    _log("generated", t0)
     # device group-by references (exact integers; the float sum by bincount)
     count = torch.bincount(pk, minlength=P)
+    _log("count", t0)
     pair = torch.unique(pid * P + pk)
+    _log(f"{pair.numel()} distinct pairs", t0)
     rows = torch.bincount(pair % P, minlength=P)
     pairs_per_pid = torch.bincount(pair // P, minlength=U)
     del pair
-    s = torch.bincount(pk, weights=val.clamp(0.0, 10.0), minlength=P)
-    torch.cuda.synchronize()
+    _log("rows", t0)
+    # the float sums on the host: a weighted device bincount funnels ~1e8
+    # float64 atomic adds into the hottest Zipf partition (minutes)
+    s = np.bincount(pk.cpu().numpy(), weights=val.clamp(0.0, 10.0).cpu().numpy(), minlength=P)
+    s = torch.from_numpy(s).to(dev)
+    _log("reference group-by", t0)
     yield dict(pid=pid, pk=pk, val=val, count=count, rows=rows, sum=s,
                pairs_per_pid=pairs_per_pid)
     torch.cuda.empty_cache()
@@ -59,9 +76,10 @@ def _partials(d, mpc, mcpp):
     acc.compute_budgets()
     res.noise_enabled = False
     res.nonce = 77
+    t0 = time.perf_counter()
     out = res.materialize(gather=False)
     got = {k: v for k, v in res.last_partials.items() if v is not None}
-    torch.cuda.synchronize()
+    _log(f"aggregate mpc {mpc} mcpp {mcpp}", t0)
     return res, out, got
 
 
