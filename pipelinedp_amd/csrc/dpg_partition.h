@@ -643,49 +643,34 @@ __device__ __forceinline__ uint32_t block_scan_digits_t(const uint32_t *cnt, uin
     return total;
 }
 
-// Scatter's per-sub-tile digit scan, in two halves around the staging of
-// the sub-tile (k_scatter):
-//
-// scatter_scan_begin: dstart[0, F] <- exclusive prefix of cnt (dstart[F] =
-// total), cnt[d] = 0; grouped / piece mode (goff: the group's digit offsets,
-// or the cursors of the fixed-capacity piece regions) also ISSUES the
-// sub-tile's run reservation of every digit it holds -- one atomic add per
-// digit, unconditional (a count of 0 adds 0) so that both of a thread's
-// atomics are in flight together -- and keeps the returned offsets in
-// registers (ScanRes).  Two barriers: the wave totals' buffer is next
-// written one sub-tile later, behind the caller's own barriers.
-//
-// scatter_scan_finish (after the staging, before the barrier that precedes
-// the write-out): cur[d] += reserved start + cnt[d] (grouped), += cnt[d]
-// (plain); the write-out then addresses cur[d] - dstart[d + 1] + k.  Piece
-// mode (kCap): a run that does not fit its region raises err bit 16 and
-// goes to the dump area at `dump` instead (the host redoes the level with
-// the histogram path).
-//
-// Round 3/4 form: the reservation atomics sat inside the scan, each behind
-// its own branch whose s_waitcnt vmcnt(0) waited for the returned offset
-// before the next was issued -- two serialised atomic round trips per
-// sub-tile on the critical path of the level-1 scatter.
-template <int DPT>
-struct ScanRes {
-    uint32_t c[DPT], o[DPT], e[DPT];
-};
-template <int T, int DPT>
-__device__ __forceinline__ uint32_t scatter_scan_begin(uint32_t *cnt, uint32_t *dstart, uint32_t F,
-                                                       uint32_t *sh16, uint32_t *goff,
-                                                       ScanRes<DPT> &sr) {
+// Scatter's per-sub-tile digit scan: dstart[0, F] <- exclusive prefix of
+// cnt (dstart[F] = total), and for every digit cur[d] += cnt[d], cnt[d] = 0
+// (the write-out then addresses cur[d] - dstart[d + 1] + k).  Grouped mode
+// (goff: the group's digit offsets): the sub-tile reserves its run of every
+// digit it holds inside its group by one atomic add, cur[d] += reserved
+// start + cnt[d].  Each reservation sits behind its own branch (its
+// s_waitcnt vmcnt(0) waits for the returned offset before the next is
+// issued): issuing a thread's two atomics together, unconditionally, costs
+// the level-1 scatter 10 more spilled VGPRs (6 -> 16), and keeping the
+// offsets in registers until after the staging measured 7.1 -> 7.55 ms
+// (round 5, profiles/r5/r5c_ab.txt).  Two barriers: the wave totals' buffer is
+// next written one sub-tile later, behind the caller's own barriers.  Piece
+// mode (kCap): goff are the cursors of fixed-capacity regions; a run that
+// does not fit raises err bit 16 and goes to the dump area at `dump` instead
+// (the host redoes the level with the histogram path).
+template <int T, int DPT, bool kCap = false>
+__device__ __forceinline__ uint32_t scatter_scan_update(uint32_t *cnt, uint32_t *dstart,
+                                                        uint32_t *cur, uint32_t F,
+                                                        uint32_t *sh16, uint32_t *goff = nullptr,
+                                                        uint32_t cap = 0, uint32_t dump = 0,
+                                                        uint32_t *err = nullptr) {
     constexpr int NW = T / 64;
     const uint32_t d0 = DPT * threadIdx.x;
-    uint32_t x = 0;
+    uint32_t c[DPT], x = 0;
 #pragma unroll
     for (int u = 0; u < DPT; ++u) {
-        sr.c[u] = d0 + u < F ? cnt[d0 + u] : 0u;
-        x += sr.c[u];
-    }
-    if (goff) {
-#pragma unroll
-        for (int u = 0; u < DPT; ++u)
-            sr.o[u] = atomicAdd(&goff[min(d0 + u, F - 1)], sr.c[u]);
+        c[u] = d0 + u < F ? cnt[d0 + u] : 0u;
+        x += c[u];
     }
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     uint32_t wt;
@@ -701,41 +686,30 @@ __device__ __forceinline__ uint32_t scatter_scan_begin(uint32_t *cnt, uint32_t *
     }
 #pragma unroll
     for (int u = 0; u < DPT; ++u) {
-        sr.e[u] = e;
         if (d0 + u < F) {
             dstart[d0 + u] = e;
+            if constexpr (kCap) {
+                if (c[u]) {
+                    const uint32_t o = atomicAdd(&goff[d0 + u], c[u]);
+                    if (o + c[u] <= cap) {
+                        cur[d0 + u] += o + c[u];
+                    } else {
+                        cur[d0 + u] = dump + e + c[u];
+                        atomicOr(err, 16u);
+                    }
+                }
+            } else if (goff) {
+                if (c[u]) cur[d0 + u] += atomicAdd(&goff[d0 + u], c[u]) + c[u];
+            } else {
+                cur[d0 + u] += c[u];
+            }
             cnt[d0 + u] = 0;
         }
-        e += sr.c[u];
+        e += c[u];
     }
     if (threadIdx.x == 0) dstart[F] = total;
     __syncthreads();
     return total;
-}
-template <int DPT, bool kCap = false>
-__device__ __forceinline__ void scatter_scan_finish(uint32_t *cur, uint32_t F, const uint32_t *goff,
-                                                    const ScanRes<DPT> &sr, uint32_t cap = 0,
-                                                    uint32_t dump = 0, uint32_t *err = nullptr) {
-    const uint32_t d0 = DPT * threadIdx.x;
-#pragma unroll
-    for (int u = 0; u < DPT; ++u) {
-        if (d0 + u >= F) continue;
-        const uint32_t c = sr.c[u];
-        if constexpr (kCap) {
-            if (c) {
-                if (sr.o[u] + c <= cap) {
-                    cur[d0 + u] += sr.o[u] + c;
-                } else {
-                    cur[d0 + u] = dump + sr.e[u] + c;
-                    atomicOr(err, 16u);
-                }
-            }
-        } else if (goff) {
-            if (c) cur[d0 + u] += sr.o[u] + c;
-        } else {
-            cur[d0 + u] += c;
-        }
-    }
 }
 
 // grid S: base[s][d] = seg_start[s] + exclusive_prefix_d(tot[s][.])  (F <= 4096)
@@ -813,17 +787,34 @@ __device__ __forceinline__ T from_words(const Words<T> &x) {
 // LDS bytes of one k_scatter instantiation (one dummy staging slot past the
 // sub-tile for records that are dropped).
 template <class Src, class Rec, int IPT, int FMAX>
-constexpr size_t scatter_lds() {
+constexpr size_t scatter_lds_core() {
     return (size_t)sizeof(Rec) * (kScatThreads * IPT + 1) +
            (Src::kDigitFromRec ? 0 : a16((size_t)2 * (kScatThreads * IPT + 1))) +
            (size_t)FMAX * 12 + 80;
+}
+// Grouped / piece modes keep the current segment's digit bases in LDS
+// (lbase, FMAX u32) when they fit beside the staging area: every tile of a
+// grouped level then starts its runs from LDS instead of FMAX global loads
+// whose vmcnt wait also drained the previous write-out's stores and the
+// next sub-tile's prefetched loads (level 1 has one sub-tile per tile).
+#ifndef DPG_SCAT_LBASE
+#define DPG_SCAT_LBASE 1
+#endif
+template <class Src, class Rec, int IPT, int FMAX>
+constexpr bool scatter_lbase() {
+    return scatter_lds_core<Src, Rec, IPT, FMAX>() + (size_t)FMAX * 4 <= 160 * 1024;
+}
+template <class Src, class Rec, int IPT, int FMAX>
+constexpr size_t scatter_lds() {
+    return scatter_lds_core<Src, Rec, IPT, FMAX>() +
+           (scatter_lbase<Src, Rec, IPT, FMAX>() ? (size_t)FMAX * 4 : 0);
 }
 
 // Phase clock of k_scatter (timing build only, -DDPG_PHASE_TIMING): wave 0
 // of every workgroup stamps s_memtime at the phase boundaries of each
 // sub-tile and adds its totals to g_scat_cyc at exit: [0] loop top ->
 // ranked (load waits + decode + LDS ranking + barrier), [1] digit scan
-// (+ reservations issued), [2] staging + reservations consumed + barrier,
+// and run reservations, [2] staging + barrier,
 // [3] next loads issued + write-out, [4] tile transitions, [5] sub-tiles.
 #ifdef DPG_PHASE_TIMING
 __device__ unsigned long long g_scat_cyc[8];
@@ -873,6 +864,9 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
     uint32_t *dstart = cnt + FMAX;
     uint32_t *cur = dstart + FMAX + 1;  // output positions (n < 2^32 per device)
     uint32_t *sh16 = cur + FMAX;
+    constexpr bool kLB = DPG_SCAT_LBASE && scatter_lbase<Src, Rec, IPT, FMAX>();
+    uint32_t *lbase = reinterpret_cast<uint32_t *>(smem + scatter_lds_core<Src, Rec, IPT, FMAX>());
+    uint32_t lseg = 0xFFFFFFFFu;  // segment whose bases lbase holds
 
     // persistent over the tiles.  XCD-local mode (xq.q): workgroup b serves
     // the queue of XCD b % 8 (round-robin placement), taking the next tile id
@@ -960,10 +954,22 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
     const uint32_t gsel = kPc ? (blockIdx.x & 7u) : td.pad;
     const uint32_t bsel = kPc ? (blockIdx.x & 7u) : td.seg;
     uint32_t *gof = goff ? goff + (size_t)gsel * F : nullptr;
-    for (uint32_t d = tid; d < F; d += kScatThreads) {
-        cur[d] = (uint32_t)(base[(size_t)bsel * F + d] +
-                            (goff ? 0u : off[(size_t)t * F + d] + (cb ? cb[d] : 0u)));
-        cnt[d] = 0;
+    if (kLB && goff) {
+        // a thread reads back only the lbase entries it wrote itself
+        if (bsel != lseg) {
+            for (uint32_t d = tid; d < F; d += kScatThreads) lbase[d] = (uint32_t)base[(size_t)bsel * F + d];
+            lseg = bsel;
+        }
+        for (uint32_t d = tid; d < F; d += kScatThreads) {
+            cur[d] = lbase[d];
+            cnt[d] = 0;
+        }
+    } else {
+        for (uint32_t d = tid; d < F; d += kScatThreads) {
+            cur[d] = (uint32_t)(base[(size_t)bsel * F + d] +
+                                (goff ? 0u : off[(size_t)t * F + d] + (cb ? cb[d] : 0u)));
+            cnt[d] = 0;
+        }
     }
     __syncthreads();
     uint32_t tn = kNone;
@@ -1006,10 +1012,8 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
         if (xq.q && tid == 0 && sb == td.begin) sh_next = nq;
         __syncthreads();
         DPG_SCAT_MARK(0);
-        constexpr int kDPT = FMAX / kScatThreads;
-        ScanRes<kDPT> sres;
-        const uint32_t total =
-            scatter_scan_begin<kScatThreads, kDPT>(cnt, dstart, F, sh16, gof, sres);
+        const uint32_t total = scatter_scan_update<kScatThreads, FMAX / kScatThreads, kPc>(
+            cnt, dstart, cur, F, sh16, gof, pcap, pdump, perr);
         DPG_SCAT_MARK(1);
         {
             uint32_t ds[IPT];
@@ -1022,8 +1026,6 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
                 if constexpr (kSD) sdig[pos] = (uint16_t)(dr[j] & 0xFFFu);
             }
         }
-        // the reservations' offsets have returned while the sub-tile was staged
-        scatter_scan_finish<kDPT, kPc>(cur, F, gof, sres, pcap, pdump, perr);
         __syncthreads();
         DPG_SCAT_MARK(2);
         const int64_t nb = sb + SUB;

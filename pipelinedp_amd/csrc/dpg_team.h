@@ -32,7 +32,10 @@ namespace dpg {
 
 constexpr int kTeamIPT = 16;                       // records per thread
 #ifndef DPG_TEAM_PF
-#define DPG_TEAM_PF 0  // experiment: next share loaded during the barrier + write-out
+#define DPG_TEAM_PF 1  // next share loaded during the barrier + write-out (same-box A/B, config 2: 5.09 -> 4.39 ms)
+#endif
+#ifndef DPG_TEAM_PF_PC
+#define DPG_TEAM_PF_PC 1  // the same for the histogram-free level 1's pieces
 #endif
 #ifndef DPG_TEAM_WB
 #define DPG_TEAM_WB 4  // staged records per thread per write-out batch
@@ -242,25 +245,33 @@ __global__ __launch_bounds__(kScatThreads) void k_part2_team(SrcAoS<R> src,
         vmask = vm;
     };
     uint32_t k = 0;  // buckets done = team barriers passed
-    // kPF (contiguous buckets): the share of this member's next non-empty
-    // bucket is loaded during the current bucket's team barrier and
-    // write-out (the local staging moves before the barrier, which frees
-    // the record registers); pf_s = the bucket those registers hold
-    constexpr bool kPF = !kPc && DPG_TEAM_PF;
+    // kPF: the share of this member's next non-empty bucket (piece mode: its
+    // piece descriptors too) is loaded during the current bucket's team
+    // barrier and write-out (the local staging moves before the barrier,
+    // which frees the record registers); pf_s = the bucket those registers
+    // hold
+    constexpr bool kPF = DPG_TEAM_PF && (!kPc || DPG_TEAM_PF_PC);
     auto next_nonempty = [&](uint32_t s) -> uint32_t {
         for (; s < S; s += 8)
-            if (__builtin_amdgcn_readfirstlane(seg_cnt[s]) != 0) break;
+            if (__builtin_amdgcn_readfirstlane(kPc ? pt.ptot[s] : seg_cnt[s]) != 0) break;
         return s;
+    };
+    // the loads of one share (piece mode: its 8-piece descriptors first)
+    auto load_share = [&](uint32_t s) {
+        int64_t st;
+        uint32_t n, b0, lim;
+        share(s, st, n, b0, lim);
+        if constexpr (kPc) {
+            vmask = 0;
+            if (lim > 0) load_pieces(s, b0, lim);
+        } else {
+            load(st + b0, lim);
+        }
     };
     uint32_t pf_s = S;
     if constexpr (kPF) {
         pf_s = next_nonempty(team);
-        if (pf_s < S) {
-            int64_t st;
-            uint32_t n, b0, lim;
-            share(pf_s, st, n, b0, lim);
-            load(st + b0, lim);
-        }
+        if (pf_s < S) load_share(pf_s);
     }
     for (uint32_t s = team; s < S; s += 8) {
         int64_t st;
@@ -276,12 +287,7 @@ __global__ __launch_bounds__(kScatThreads) void k_part2_team(SrcAoS<R> src,
         }
         uint32_t *tt = ts.tot + ((size_t)team * 3 + k % 3) * F;
         // ---- load + rank
-        if constexpr (kPc) {
-            vmask = 0;
-            if (lim > 0) load_pieces(s, b0, lim);
-        } else if constexpr (!kPF) {
-            load(st + b0, lim);
-        }
+        if constexpr (!kPF) load_share(s);
         uint32_t dr[IPT];
         uint32_t nv = 0;  // records of the share (lim less the padding)
         {
@@ -348,12 +354,7 @@ __global__ __launch_bounds__(kScatThreads) void k_part2_team(SrcAoS<R> src,
         }
         auto prefetch = [&]() {
             if constexpr (kPF) {
-                if (pf_s < S) {
-                    int64_t st2;
-                    uint32_t n2, b2, lim2;
-                    share(pf_s, st2, n2, b2, lim2);
-                    load(st2 + b2, lim2);
-                }
+                if (pf_s < S) load_share(pf_s);
             }
         };
         if (!team_barrier(ts, team, T * k, &sh_ok, prefetch)) return;
