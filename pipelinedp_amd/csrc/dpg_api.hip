@@ -298,6 +298,45 @@ int agg_bits() {
 // per-tile histograms of the plain XCD-local mode cost 667 MB of traffic and
 // scans per 1e9 records.  Order inside a digit is arrival order (nothing
 // downstream depends on it, DESIGN.md "Randomness").
+// Timing build (DPG_PHASE_TIMING=1 at run time): k_scatter's phase clock
+// (dpg_partition.h g_scat_cyc) around one launch, printed per workgroup.
+int scat_phase_begin(dpg_ctx *ctx, hipStream_t s) {
+#ifdef DPG_PHASE_TIMING
+    if (std::getenv("DPG_PHASE_TIMING")) {
+        unsigned long long z[8] = {};
+        if (hipMemcpyToSymbolAsync(HIP_SYMBOL(g_scat_cyc), z, sizeof(z), 0, hipMemcpyHostToDevice,
+                                   s) != hipSuccess)
+            return fail(ctx, DPG_ERR_HIP, "scatter phase clock");
+    }
+#else
+    (void)ctx;
+    (void)s;
+#endif
+    return DPG_OK;
+}
+int scat_phase_end(dpg_ctx *ctx, hipStream_t s, const char *tag, uint32_t gs) {
+#ifdef DPG_PHASE_TIMING
+    if (std::getenv("DPG_PHASE_TIMING")) {
+        unsigned long long h[8];
+        if (hipMemcpyFromSymbolAsync(h, HIP_SYMBOL(g_scat_cyc), sizeof(h), 0, hipMemcpyDeviceToHost,
+                                     s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return fail(ctx, DPG_ERR_HIP, "scatter phase clock");
+        static const char *nm[5] = {"rank", "scan", "stage", "write", "tile"};
+        std::fprintf(stderr, "[dpg] %s scatter phases (wave-0 cycles per workgroup, %u WGs, "
+                             "%.1f sub-tiles each):", tag, gs, (double)h[5] / gs);
+        for (int k = 0; k < 5; ++k) std::fprintf(stderr, " %s %.0f", nm[k], (double)h[k] / gs);
+        std::fprintf(stderr, "\n");
+    }
+#else
+    (void)ctx;
+    (void)s;
+    (void)tag;
+    (void)gs;
+#endif
+    return DPG_OK;
+}
+
 template <class Src, class Rec, int IPT, int FMAX>
 int run_level_grouped(dpg_ctx *ctx, hipStream_t s, const Src &src, uint32_t S,
                       const int64_t *seg_start, const uint32_t *seg_cnt, const int64_t *seg_cnt64,
@@ -373,30 +412,11 @@ int run_level_grouped(dpg_ctx *ctx, hipStream_t s, const Src &src, uint32_t S,
                               (int)lds);
     stage(ctx, s, (t + ":scatter").c_str());
     const uint32_t gs = std::min<uint32_t>(max_subs, (uint32_t)ctx->n_cu);  // one per CU
-#ifdef DPG_PHASE_TIMING
-    const bool ptime = std::getenv("DPG_PHASE_TIMING") != nullptr;
-    if (ptime) {
-        unsigned long long z[8] = {};
-        HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_scat_cyc), z, sizeof(z), 0,
-                                       hipMemcpyHostToDevice, s));
-    }
-#endif
+    if (int r = scat_phase_begin(ctx, s)) return r;
     kern<<<gs, kScatThreads, lds, s>>>(src, tiles, ntiles_dev, F, bits, nullptr, base, out, xq,
                                        nullptr, nullptr, nullptr, 1u, hist, 0u, 0u, nullptr);
     LAUNCH_CHECK();
-#ifdef DPG_PHASE_TIMING
-    if (ptime) {
-        unsigned long long h[8];
-        HIP_TRY(hipMemcpyFromSymbolAsync(h, HIP_SYMBOL(g_scat_cyc), sizeof(h), 0,
-                                         hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
-        static const char *nm[5] = {"rank", "scan", "stage", "write", "tile"};
-        std::fprintf(stderr, "[dpg] %s scatter phases (wave-0 cycles per workgroup, %u WGs, "
-                             "%.1f sub-tiles each):", tag, gs, (double)h[5] / gs);
-        for (int k = 0; k < 5; ++k) std::fprintf(stderr, " %s %.0f", nm[k], (double)h[k] / gs);
-        std::fprintf(stderr, "\n");
-    }
-#endif
+    if (int r = scat_phase_end(ctx, s, tag, gs)) return r;
     *base_out = base;
     *tot_out = tot;
     return DPG_OK;
@@ -1160,10 +1180,12 @@ int run_level1_pieces(dpg_ctx *ctx, hipStream_t s, const SrcSoAKey<R, true> &src
     (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
     const uint32_t gs = std::min<uint32_t>(nt, (uint32_t)ctx->n_cu);  // one per CU
+    if (int r = scat_phase_begin(ctx, s)) return r;
     kern<<<gs, kScatThreads, lds, s>>>(src, tiles, &ctl->ntiles[0], F, bits, nullptr, rbase, out,
                                        XcdQueues{}, nullptr, nullptr, nullptr, 1u, cum, C,
                                        (uint32_t)((uint64_t)8 * F * C), &ctl->err);
     LAUNCH_CHECK();
+    if (int r = scat_phase_end(ctx, s, "partition1:pieces", gs)) return r;
     k_piece_totals<<<1, 1024, 0, s>>>(cum, F, tot, ptot, ostart);
     LAUNCH_CHECK();
     // totals and the error word reach the host for the overflow / team checks
@@ -1286,15 +1308,19 @@ int pipeline(dpg_ctx *ctx, hipStream_t s, const int64_t *pid, const int64_t *pk,
     // level 1 without a histogram pass (k_scatter's piece mode, dpg_team.h
     // PieceTab): 8-byte records whose level 2 runs by teams; every XCD
     // appends to fixed-capacity regions, so recA holds 8 F1 regions of
-    // `pcap` records (+ a dump area).  Opt-in (DPG_L1_PIECES=1): same-box
-    // A/B at config 2, level 1 8.8 -> 7.4 ms but the team level 2 reading
-    // the pieces 5.1 -> 6.8 ms, a net loss.
+    // `pcap` records (+ a dump area).  The default since round 5
+    // (DPG_L1_PIECES=0: the histogram path): with the team level 2 loading
+    // the next bucket's pieces during its barrier and write-out, same-box
+    // A/B at config 2 22.07-22.26 -> 21.42-21.44 ms per step (level 1 1.46 +
+    // 7.08 -> 7.35 ms, team 4.42-4.49 -> 4.93 ms; profiles/r5/r5d_ab.txt).
+    // Round 4, without that prefetch, measured it a net loss (team 5.1 ->
+    // 6.8 ms).
     constexpr int kIptPc = DPG_IPT_PC;
     const int64_t subPc = (int64_t)kScatThreads * kIptPc;
     uint32_t pcap = 0;
     bool pieces = false;
     if constexpr (sizeof(R) == 8) {
-        if (team && env_int("DPG_L1_PIECES", 0) != 0 && n >= ((int64_t)1 << 22) &&
+        if (team && env_int("DPG_L1_PIECES", 1) != 0 && n >= ((int64_t)1 << 22) &&
             pl.b1 > (uint32_t)agg_bits()) {
             pcap = piece_capacity(n, F1, subPc);
             pieces = pcap > 0;

@@ -1082,7 +1082,16 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
             // (non-temporal loads / stores measured slower: the partial
             // lines of the runs merge in L2)
 #pragma unroll
+#if DPG_EXP_SCAT_NOSTORE  // diagnostic only (wrong results): the scatter without its stores
+            for (int u = 0; u < WB; ++u) {
+                uint32_t w0;
+                __builtin_memcpy(&w0, &x[u], 4);
+                if (w0 == 0x12345u && c1[u] == 0x777u)  // (never)
+                    *reinterpret_cast<W *>(&out[c1[u] - c2[u] + kc[u]]) = x[u];
+            }
+#else
             for (int u = 0; u < WB; ++u) *reinterpret_cast<W *>(&out[c1[u] - c2[u] + kc[u]]) = x[u];
+#endif
         }
         // the next sub-tile's first barrier (after its ranking) orders this
         // write-out's LDS reads before the next scan and staging

@@ -97,11 +97,11 @@ def test_config2_bounding_triggered_matches_oracle(built, config2_data):
 def test_config2_level2_paths_match_oracle(built, config2_data, monkeypatch, mode):
     """The first two partition levels five ways, every one bit-exact against
     the oracle (kept pairs, counts; sums to 1e-9):
-    team -- the default for 8-byte records: level 1 with its histogram,
-      level 2 by teams without one;
-    pieces -- level 1 without a histogram pass too (DPG_L1_PIECES=1:
-      per-XCD fixed-capacity regions, k_scatter's piece mode), level 2 by
-      teams reading the pieces;
+    pieces -- the default for 8-byte records (round 5): level 1 without a
+      histogram pass (per-XCD fixed-capacity regions, k_scatter's piece
+      mode), level 2 by teams reading the pieces;
+    team -- level 1 with its histogram (DPG_L1_PIECES=0), level 2 by teams
+      without one;
     grouped -- both levels with histograms (DPG_TEAM_L2=0);
     team_abort -- pieces, and a team barrier that gives up (test hook
       DPG_DEBUG_TEAM_ABORT: abort flag + err bit 8, as after a timeout); the
@@ -112,8 +112,8 @@ def test_config2_level2_paths_match_oracle(built, config2_data, monkeypatch, mod
       the host redoes level 1 with its histogram before level 2."""
     if mode == "grouped":
         monkeypatch.setenv("DPG_TEAM_L2", "0")
-    if mode in ("pieces", "team_abort", "piece_overflow"):
-        monkeypatch.setenv("DPG_L1_PIECES", "1")
+    monkeypatch.setenv("DPG_L1_PIECES", "1" if mode in ("pieces", "team_abort", "piece_overflow")
+                       else "0")
     if mode == "team_abort":
         monkeypatch.setenv("DPG_DEBUG_TEAM_ABORT", "1")
     if mode == "piece_overflow":
