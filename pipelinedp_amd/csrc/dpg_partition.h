@@ -658,6 +658,12 @@ __device__ __forceinline__ uint32_t block_scan_digits_t(const uint32_t *cnt, uin
 // mode (kCap): goff are the cursors of fixed-capacity regions; a run that
 // does not fit raises err bit 16 and goes to the dump area at `dump` instead
 // (the host redoes the level with the histogram path).
+#ifndef DPG_SCAT_RSV_PAIR
+#define DPG_SCAT_RSV_PAIR 1
+#endif
+#ifndef DPG_SCAT_RSV_PAIR_EARLY
+#define DPG_SCAT_RSV_PAIR_EARLY 1
+#endif
 template <int T, int DPT, bool kCap = false>
 __device__ __forceinline__ uint32_t scatter_scan_update(uint32_t *cnt, uint32_t *dstart,
                                                         uint32_t *cur, uint32_t F,
@@ -672,6 +678,20 @@ __device__ __forceinline__ uint32_t scatter_scan_update(uint32_t *cnt, uint32_t 
         c[u] = d0 + u < F ? cnt[d0 + u] : 0u;
         x += c[u];
     }
+    // two digits per thread (F even): one 64-bit atomic reserves both runs
+    // (the two 32-bit cursors sit in one aligned word; a cursor stays far
+    // below 2^32, so the low add never carries into the high one)
+    constexpr bool kPair = DPT == 2 && DPG_SCAT_RSV_PAIR;
+    uint32_t o[DPT];
+    if constexpr (kPair && DPG_SCAT_RSV_PAIR_EARLY) {
+        if (goff && d0 < F) {
+            const unsigned long long old = atomicAdd(
+                reinterpret_cast<unsigned long long *>(&goff[d0]),
+                (unsigned long long)c[0] | ((unsigned long long)c[1] << 32));
+            o[0] = (uint32_t)old;
+            o[1] = (uint32_t)(old >> 32);
+        }
+    }
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     uint32_t wt;
     uint32_t e = wave_excl_scan(x, wt);
@@ -684,22 +704,31 @@ __device__ __forceinline__ uint32_t scatter_scan_update(uint32_t *cnt, uint32_t 
         if (k < w) e += y;
         total += y;
     }
+    if constexpr (kPair && !DPG_SCAT_RSV_PAIR_EARLY) {
+        if (goff && d0 < F) {
+            const unsigned long long old = atomicAdd(
+                reinterpret_cast<unsigned long long *>(&goff[d0]),
+                (unsigned long long)c[0] | ((unsigned long long)c[1] << 32));
+            o[0] = (uint32_t)old;
+            o[1] = (uint32_t)(old >> 32);
+        }
+    }
 #pragma unroll
     for (int u = 0; u < DPT; ++u) {
         if (d0 + u < F) {
             dstart[d0 + u] = e;
             if constexpr (kCap) {
                 if (c[u]) {
-                    const uint32_t o = atomicAdd(&goff[d0 + u], c[u]);
-                    if (o + c[u] <= cap) {
-                        cur[d0 + u] += o + c[u];
+                    const uint32_t ou = kPair ? o[u] : atomicAdd(&goff[d0 + u], c[u]);
+                    if (ou + c[u] <= cap) {
+                        cur[d0 + u] += ou + c[u];
                     } else {
                         cur[d0 + u] = dump + e + c[u];
                         atomicOr(err, 16u);
                     }
                 }
             } else if (goff) {
-                if (c[u]) cur[d0 + u] += atomicAdd(&goff[d0 + u], c[u]) + c[u];
+                if (c[u]) cur[d0 + u] += (kPair ? o[u] : atomicAdd(&goff[d0 + u], c[u])) + c[u];
             } else {
                 cur[d0 + u] += c[u];
             }
