@@ -104,6 +104,33 @@ __device__ __forceinline__ double clamp_f64(double x, double lo, double hi) {
     return r;
 }
 
+// clamp_f64 of a wave-uniform value held in scalar registers (one scalar
+// operand per VOP3 instruction)
+__device__ __forceinline__ double clamp_f64_s(double x, double lo, double hi) {
+    double r;
+    asm("v_max_f64 %0, %1, %2\n\tv_min_f64 %0, %0, %3" : "=&v"(r) : "s"(x), "v"(lo), "v"(hi));
+    return r;
+}
+
+// pk, cnt and sum of one pair by a scalar load: the pair is the same for
+// every configuration lane, so the accumulate loop reads them as scalar
+// operands (no LDS broadcast and no v_readfirstlane per pair).  Loads only:
+// nothing is written through the scalar cache.
+struct PairHead {
+    uint32_t pk, cnt;
+    double sum;
+};
+__device__ __forceinline__ PairHead sload_head(const ItemPA *p) {
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    u4 r;
+    asm volatile("s_load_dwordx4 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(p));
+    PairHead h;
+    h.pk = r.x;
+    h.cnt = r.y;
+    h.sum = __hiloint2double((int)r.w, (int)r.z);
+    return h;
+}
+
 __device__ __forceinline__ void ua_put(double *dst, double v, bool atomic) {
     if (atomic) atomicAdd(dst, v);
     else *dst = v;
@@ -183,26 +210,25 @@ __global__ __launch_bounds__(64) void k_ua_accumulate(const ItemPA *pairs,
         if (kCount) put5(rcd, 0.0, spci - rcd, cel, cvl);
         if (kPid) put5(rnd - nz, 0.0, 0.0, (e - rnd) + zel, v - zvl);
     };
-    // The 64 pairs of a block are broadcast to the configurations through
-    // LDS (uniform-address reads), not by readlane of the loaded registers:
+    // Per block of 64 pairs each lane computes one pair's 1 / n_partitions
+    // into LDS (one division per pair, not per (pair, configuration)); the
+    // pair's key, count and sum come by scalar loads (sload_head).  (Round 3
+    // loaded the pair into registers per lane and broadcast it by readlane:
     // with the loaded registers live in the loop, every iteration waited for
-    // all vector memory operations (s_waitcnt vmcnt(0) at the loop head),
-    // i.e. for the stores of every partition flush.
-    __shared__ uint32_t s_pk[64], s_cnt[64];
-    __shared__ double s_sum[64], s_inv[64];
+    // all vector memory operations -- s_waitcnt vmcnt(0) at the loop head --
+    // i.e. for the stores of every partition flush.  Round 4 broadcast key,
+    // count, sum and inverse through LDS: 31 VALU instructions per pair,
+    // 4 of them v_readfirstlane / address moves.)
+    __shared__ double s_inv[64];
     for (int64_t b = lo; b < hi; b += 64) {
         const int64_t i = b + c < hi ? b + c : hi - 1;
-        const ItemPA mine = pairs[i];
-        // 1 / n_partitions of the lane's pair: one division per pair instead
-        // of one per (pair, configuration)
-        s_pk[c] = mine.pk;
-        s_cnt[c] = mine.cnt;
-        s_sum[c] = mine.sum;
-        s_inv[c] = mine.npart > 0 ? 1.0 / (double)mine.npart : 0.0;
+        const uint32_t np = pairs[i].npart;
+        s_inv[c] = np > 0 ? 1.0 / (double)np : 0.0;
         __syncthreads();
         const int m = (int)(hi - b < 64 ? hi - b : 64);
         for (int j = 0; j < m; ++j) {
-            const uint32_t pk = __builtin_amdgcn_readfirstlane(s_pk[j]);
+            const PairHead h = sload_head(pairs + b + j);
+            const uint32_t pk = h.pk;
             if (pk != cur) {
                 flush(cur);
                 e = v = t = 0.0;
@@ -216,7 +242,7 @@ __global__ __launch_bounds__(64) void k_ua_accumulate(const ItemPA *pairs,
                 skip = a.sample_mask && !bit_of(a.sample_mask, cur);
             }
             if (skip) continue;
-            const uint32_t cnt = __builtin_amdgcn_readfirstlane(s_cnt[j]);
+            const uint32_t cnt = h.cnt;
             const double inv = s_inv[j];
             // l0 keep probability of this pair (per_partition_combiners.py:203-205)
             const double p = fmin(1.0, cf.mpc * inv);
@@ -228,8 +254,8 @@ __global__ __launch_bounds__(64) void k_ua_accumulate(const ItemPA *pairs,
             rn += 1;
             rc += cnt;
             if constexpr (kSum) {
-                const double x = s_sum[j];
-                const double pc = clamp_f64(x, clo, chi);
+                const double x = h.sum;
+                const double pc = clamp_f64_s(x, clo, chi);
                 es.tot += x;
                 es.cmin += fmax(clo - x, 0.0);  // pc - x where x < lo
                 es.cmax += fmin(chi - x, 0.0);  // pc - x where x > hi
@@ -243,13 +269,13 @@ __global__ __launch_bounds__(64) void k_ua_accumulate(const ItemPA *pairs,
                 cel = fma(-pc, omp, cel);
                 cvl = fma(pc * pc, q, cvl);
             }
-            if (kPid && cnt == 0) {  // wave-uniform (the pair is broadcast)
+            if (kPid && cnt == 0) {  // wave-uniform
                 nz += 1.0;
                 zel += omp;
                 zvl += q;
             }
         }
-        __syncthreads();  // the next block rewrites s_*
+        __syncthreads();  // the next block rewrites s_inv
     }
     flush(cur);
 }
