@@ -104,6 +104,14 @@ __device__ __forceinline__ double clamp_f64(double x, double lo, double hi) {
     return r;
 }
 
+// min(a, b) as one bare v_min_f64 (see clamp_f64: fmin would canonicalise
+// both operands first)
+__device__ __forceinline__ double min_f64(double a, double b) {
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 // clamp_f64 of a wave-uniform value held in scalar registers (one scalar
 // operand per VOP3 instruction)
 __device__ __forceinline__ double clamp_f64_s(double x, double lo, double hi) {
@@ -170,7 +178,7 @@ __global__ __launch_bounds__(64) void k_ua_accumulate(const ItemPA *pairs,
     double spci = 0;                   // COUNT: sum of the clipped counts (exact: < 2^53)
     double cel = 0, cvl = 0;           // COUNT: l0 mean, l0 variance
     double nz = 0, zel = 0, zvl = 0;   // pairs of count 0: number, sum 1 - p, sum q
-    const uint32_t mcpp_i = cf.mcpp >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)cf.mcpp;
+    const double mcpp_d = cf.mcpp;
     const double clo = cf.lo, chi = cf.hi;
     es.clear();
     uint32_t cur = pairs[lo].pk;
@@ -219,13 +227,16 @@ __global__ __launch_bounds__(64) void k_ua_accumulate(const ItemPA *pairs,
     // i.e. for the stores of every partition flush.  Round 4 broadcast key,
     // count, sum and inverse through LDS: 31 VALU instructions per pair,
     // 4 of them v_readfirstlane / address moves.)
-    __shared__ double s_inv[64];
+    // (1 / n_partitions, count) per pair as doubles, read by one LDS load
+    __shared__ double2 s_pair[64];
     for (int64_t b = lo; b < hi; b += 64) {
         const int64_t i = b + c < hi ? b + c : hi - 1;
         const uint32_t np = pairs[i].npart;
-        s_inv[c] = np > 0 ? 1.0 / (double)np : 0.0;
+        s_pair[c] = make_double2(np > 0 ? 1.0 / (double)np : 0.0, (double)pairs[i].cnt);
         __syncthreads();
-        const int m = (int)(hi - b < 64 ? hi - b : 64);
+        // the trip count as a scalar: a vector loop counter costs one VALU
+        // instruction per pair
+        const int m = __builtin_amdgcn_readfirstlane((int)(hi - b < 64 ? hi - b : 64));
         for (int j = 0; j < m; ++j) {
             const PairHead h = sload_head(pairs + b + j);
             const uint32_t pk = h.pk;
@@ -243,7 +254,8 @@ __global__ __launch_bounds__(64) void k_ua_accumulate(const ItemPA *pairs,
             }
             if (skip) continue;
             const uint32_t cnt = h.cnt;
-            const double inv = s_inv[j];
+            const double2 ic = s_pair[j];
+            const double inv = ic.x;
             // l0 keep probability of this pair (per_partition_combiners.py:203-205)
             const double p = fmin(1.0, cf.mpc * inv);
             const double omp = 1.0 - p;
@@ -256,15 +268,17 @@ __global__ __launch_bounds__(64) void k_ua_accumulate(const ItemPA *pairs,
             if constexpr (kSum) {
                 const double x = h.sum;
                 const double pc = clamp_f64_s(x, clo, chi);
+                // pc - x: lo - x where x < lo, hi - x where x > hi, else 0
+                const double d = pc - x;
                 es.tot += x;
-                es.cmin += fmax(clo - x, 0.0);  // pc - x where x < lo
-                es.cmax += fmin(chi - x, 0.0);  // pc - x where x > hi
+                es.cmin += fmax(d, 0.0);
+                es.cmax += fmin(d, 0.0);
                 es.el0 = fma(-pc, omp, es.el0);
                 es.vl0 = fma(pc * pc, q, es.vl0);
             }
             if constexpr (kCount) {
-                const uint32_t pci = cnt < mcpp_i ? cnt : mcpp_i;
-                const double pc = (double)pci;
+                // min(count, mcpp) on the staged double count (exact: < 2^53)
+                const double pc = min_f64(ic.y, mcpp_d);
                 spci += pc;
                 cel = fma(-pc, omp, cel);
                 cvl = fma(pc * pc, q, cvl);
@@ -275,7 +289,7 @@ __global__ __launch_bounds__(64) void k_ua_accumulate(const ItemPA *pairs,
                 zvl += q;
             }
         }
-        __syncthreads();  // the next block rewrites s_inv
+        __syncthreads();  // the next block rewrites s_pair
     }
     flush(cur);
 }
