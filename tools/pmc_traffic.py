@@ -22,6 +22,7 @@ import re
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+UNTIMED = ("k_pid_minmax",)
 
 
 def short(name: str) -> str:
@@ -79,12 +80,17 @@ def main(fetch_csv, write_csv, records, out, cal_f=None, cal_w=None, cal_j=None)
         kernels[k] = rf * fb + wf * wb
         raw[k] = {"fetch_size_bytes": fb, "write_size_bytes": wb,
                   "launches": max(f.get(k, (0,))[0], w.get(k, (0,))[0])}
+    # kernels of bench.py's untimed calls only: the privacy-id range pass
+    # (kernels.pidrange_untimed in the bench line; the timed calls declare
+    # the range) is not part of a step
+    untimed = {k: v for k, v in kernels.items() if k in UNTIMED}
     res = {"records": int(records), "lib_sha256": lib_sha(),
            "correction": (f"{rf:.3f} x FETCH_SIZE + {wf:.3f} x WRITE_SIZE (factors measured "
                           f"on 8-B/lane streaming loads / stores, tools/calib_fetch.hip)"
                           if cal else "2 x FETCH_SIZE + WRITE_SIZE (guide's 16-B/lane rule)"),
            "calibration": cal, "kernels": kernels, "raw": raw,
-           "bytes_per_step": sum(kernels.values())}
+           "untimed_kernels": sorted(untimed),
+           "bytes_per_step": sum(v for k, v in kernels.items() if k not in UNTIMED)}
     json.dump(res, open(out, "w"), indent=1)
     if cal:
         print("calibration:", {k: round(v, 3) for k, v in cal.items() if k != "raw"})
