@@ -247,7 +247,9 @@ class DeviceAggregation:
             kept_out = torch.empty(max(local_P * n_out, 1), **f64)
             k = ctx.compact(keep.data_ptr(), out.data_ptr(), local_P, n_out, ids.data_ptr(),
                             kept_out.data_ptr(), sptr)
-            ids = ids[:k] * pk_stride + pk_offset
+            ids = ids[:k]
+            if pk_stride != 1 or pk_offset:  # several ranks: this rank's slice
+                ids = ids * pk_stride + pk_offset
             vals = kept_out[:k * n_out].view(k, n_out) if n_out else torch.empty((k, 0), **f64)
             if backend.world_size > 1 and gather:
                 ids, vals = distributed.all_gather_results(ids, vals, backend.process_group)
