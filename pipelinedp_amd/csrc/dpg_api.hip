@@ -1964,9 +1964,26 @@ int dpg_utility_analysis(dpg_ctx *ctx, const dpg_pair_entry *pairs,
         cls[i] = k;
     }
     a.n_cls = (int32_t)cls_rep.size();
-    // pi(0 .. npi - 1) per class in <= 32 KB of LDS (4 waves per CU), at
-    // least the exact PMF's 104 counts
-    a.npi = (int32_t)std::max<int64_t>(kPgfB * kPgfNB, (32 * 1024 / 8) / a.n_cls);
+    // pi(0 .. npi - 1) per class in LDS: at least the exact PMF's 104
+    // counts, at most 32 KB, and no further than the last count whose keep
+    // probability is below 1 (ua_pi_range; beyond it the normal
+    // approximation telescopes without reading pi): the smaller the table,
+    // the more waves of k_ua_select share a CU
+    int64_t top = 0;
+    for (int k = 0; k < a.n_cls; ++k) {
+        const UaConfig &r = hc[cls_rep[k]];
+        const int64_t sh = r.pre_threshold > 0 ? r.pre_threshold - 1 : 0;
+        int64_t i1;
+        if (r.strategy == DPG_SELECT_TRUNCATED_GEOMETRIC)
+            i1 = r.table_len - 1 + sh;
+        else if (r.strategy == DPG_SELECT_LAPLACE_THRESHOLD)
+            i1 = (int64_t)std::ceil(r.threshold + 37.5 * r.scale) + sh;
+        else
+            i1 = (int64_t)std::ceil(r.threshold + 8.5 * r.scale) + sh;
+        top = std::max(top, i1 + 1);
+    }
+    a.npi = (int32_t)std::max<int64_t>(
+        kPgfB * kPgfNB, std::min<int64_t>(top, (32 * 1024 / 8) / a.n_cls));
     WS(dcls, int32_t, "ua.cls", C + cls_rep.size());
     std::vector<int32_t> hcls(cls);
     hcls.insert(hcls.end(), cls_rep.begin(), cls_rep.end());
@@ -2017,18 +2034,26 @@ int dpg_utility_analysis(dpg_ctx *ctx, const dpg_pair_entry *pairs,
         LAUNCH_CHECK();
     } else if (n > 0) {
         stage(ctx, s, "ua.select");
-        const unsigned g = (unsigned)std::min<int64_t>(P, (int64_t)ctx->n_cu * 16);
         const size_t lds = (size_t)a.npi * a.n_cls * 8;
-        // lanes per selection class of the exact PMF (dpg_utility.h)
-        auto launch = [&](auto kern) {
+        // the exact-PMF partitions (<= 100 pairs) in a pass of their own
+        // with a 104-count pi table (its LDS share allows several times the
+        // resident waves of the full table), then the others
+        const size_t lds_x = (size_t)kPgfB * kPgfNB * a.n_cls * 8;
+        auto launch = [&](auto kern, size_t l) {
             (void)hipFuncSetAttribute((const void *)kern,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            kern<<<g, 64, lds, s>>>(reinterpret_cast<const ItemPA *>(pairs), partition_start, a);
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)l);
+            int occ = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void *)kern, 64, l) !=
+                    hipSuccess || occ < 1)
+                occ = 4;
+            const unsigned g = (unsigned)std::min<int64_t>(P, (int64_t)ctx->n_cu * occ);
+            kern<<<g, 64, l, s>>>(reinterpret_cast<const ItemPA *>(pairs), partition_start, a);
         };
-        if (a.n_cls <= 8) launch(k_ua_select<8>);
-        else if (a.n_cls <= 16) launch(k_ua_select<4>);
-        else if (a.n_cls <= 32) launch(k_ua_select<2>);
-        else launch(k_ua_select<1>);
+        // lanes per selection class of the exact PMF (dpg_utility.h)
+        if (a.n_cls <= 8) launch(k_ua_select<8, 1>, lds_x), launch(k_ua_select<8, 2>, lds);
+        else if (a.n_cls <= 16) launch(k_ua_select<4, 1>, lds_x), launch(k_ua_select<4, 2>, lds);
+        else if (a.n_cls <= 32) launch(k_ua_select<2, 1>, lds_x), launch(k_ua_select<2, 2>, lds);
+        else launch(k_ua_select<1>, lds);
         LAUNCH_CHECK();
     }
     if (report) {

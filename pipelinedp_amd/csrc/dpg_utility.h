@@ -371,18 +371,25 @@ __device__ __forceinline__ void ua_pi_range(const UaConfig &cf, int64_t &i0, int
 // the class's LPC lanes and every configuration lane reads its class's
 // value.  (Per configuration, the 104 coefficients held 208 VGPRs, one wave
 // per SIMD.)
-template <int LPC>
+//
+// kPart: 0 every partition; 1 the exact-PMF partitions only (<= 100 pairs,
+// LPC > 1), with pi tabled for the 104 counts the PMF can reach (6.5 KB of
+// LDS per wave at 8 classes instead of up to 32 KB: one partition per wave
+// is latency-bound, so resident waves count); 2 the others (normal
+// approximation, the full table).
+template <int LPC, int kPart = 0>
 __global__ __launch_bounds__(64) void k_ua_select(const ItemPA *pairs, const int64_t *pstart,
                                                   UaArgs a) {
     extern __shared__ __attribute__((aligned(16))) double spi[];
     constexpr int NCO = kPgfB * kPgfNB;
     constexpr int CPL = (NCO + LPC - 1) / LPC;
+    static_assert(kPart != 1 || LPC > 1, "exact-only pass needs the class-shared PMF");
     __shared__ double s_inv[kUaMaxExact + 28];
     const int c = (int)__lane_id();
     const int64_t C64 = a.n_configs;
     const bool lane_on = c < a.n_configs;
     const UaConfig cf = a.cfg[lane_on ? c : 0];
-    const int K = a.n_cls, NPI = a.npi;
+    const int K = a.n_cls, NPI = kPart == 1 ? NCO : a.npi;
     for (int x = c; x < NPI * K; x += 64) {
         const int i = x / K, kc = x - i * K;
         spi[x] = ua_pi(a.cfg[a.cls_rep[kc]], a.tables, i);
@@ -395,8 +402,10 @@ __global__ __launch_bounds__(64) void k_ua_select(const ItemPA *pairs, const int
     for (int64_t k = blockIdx.x; k < a.P; k += gridDim.x) {
         const int64_t b = pstart[k], n = pstart[k + 1] - b;
         if (n == 0 || (a.sample_mask && !bit_of(a.sample_mask, k))) continue;
+        if constexpr (kPart == 1) if (n > kUaMaxExact) continue;
+        if constexpr (kPart == 2) if (n <= kUaMaxExact) continue;
         double keep = 0.0;
-        if constexpr (LPC > 1) if (n <= kUaMaxExact) {
+        if constexpr (LPC > 1 && kPart != 2) if (n <= kUaMaxExact) {
             const int kc = c / LPC, l = c % LPC;
             const int kcs = kc < K ? kc : 0;
             const double mpc_k = a.cfg[a.cls_rep[kcs]].mpc;
@@ -431,6 +440,7 @@ __global__ __launch_bounds__(64) void k_ua_select(const ItemPA *pairs, const int
             if (lane_on) a.keep[k * C64 + c] = keep;
             continue;
         }
+        if constexpr (kPart == 1) continue;
         if (LPC == 1 && n <= kUaMaxExact) {
             // 1 / n_partitions of pairs lane and lane + 64, broadcast below
             const uint32_t n0 = pairs[b + min((int64_t)c, n - 1)].npart;
