@@ -303,6 +303,15 @@ int dpg_compact_kept(dpg_ctx *ctx, const uint8_t *keep, const double *out,
                      int64_t *kept_ids, double *kept_out, int64_t *n_kept,
                      void *stream);
 
+/* The same without the host synchronisation: info (device int64[2])
+ * receives the kept count (info[0]) and the bounding's error bits (info[1];
+ * bit 1: the internal hash-table error dpg_compact_kept reports), in stream
+ * order, so that a caller can enqueue the next release before reading them. */
+int dpg_compact_kept_async(dpg_ctx *ctx, const uint8_t *keep, const double *out,
+                           int64_t n_partitions, int32_t n_outputs,
+                           int64_t *kept_ids, double *kept_out, int64_t *info,
+                           void *stream);
+
 /* Utility-analysis pre-aggregate: no contribution bounding; one entry per
  * distinct (privacy id, partition) pair, sorted by partition key, into
  * pairs[0, *n_pairs) (device, `capacity` entries; n always suffices), and

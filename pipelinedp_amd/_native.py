@@ -17,7 +17,8 @@ ERRORS = {1: "invalid argument", 2: "key out of range", 3: "HIP error",
 EXPORTED = ("dpg_ctx_create", "dpg_ctx_destroy", "dpg_last_error", "dpg_set_seed",
             "dpg_set_tuning",
             "dpg_bound_aggregate", "dpg_select_and_noise", "dpg_compact_kept",
-            "dpg_last_stage_times", "dpg_stream_seed", "dpg_preaggregate",
+            "dpg_compact_kept_async", "dpg_last_stage_times", "dpg_stream_seed",
+            "dpg_preaggregate",
             "dpg_utility_analysis", "dpg_dataset_histograms",
             "dpg_comm_unique_id", "dpg_ctx_create_comm", "dpg_reduce_scatter_partials",
             "dpg_pack_partials", "dpg_unpack_partials", "dpg_export_error",
@@ -163,6 +164,8 @@ def load():
         lib.dpg_compact_kept.argtypes = [vp, vp, vp, i64, i32, vp, vp,
                                          ctypes.POINTER(ctypes.c_int64), vp]
         lib.dpg_compact_kept.restype = ctypes.c_int
+        lib.dpg_compact_kept_async.argtypes = [vp, vp, vp, i64, i32, vp, vp, vp, vp]
+        lib.dpg_compact_kept_async.restype = ctypes.c_int
         lib.dpg_preaggregate.argtypes = [vp, vp, vp, vp, i64, ctypes.POINTER(BoundParams), vp,
                                          i64, vp, ctypes.POINTER(ctypes.c_int64), vp]
         lib.dpg_preaggregate.restype = ctypes.c_int
@@ -306,6 +309,15 @@ class Context:
                                        ids_ptr, kept_out_ptr, ctypes.byref(n), stream)
         self.check(st, "dpg_compact_kept")
         return n.value
+
+    def compact_async(self, keep_ptr, out_ptr, n_partitions, n_out, ids_ptr, kept_out_ptr,
+                      info_ptr, stream) -> None:
+        """dpg_compact_kept without the host synchronisation: the kept count
+        and the bounding's error bits land in the device int64[2] at
+        info_ptr in stream order."""
+        st = self.lib.dpg_compact_kept_async(self.handle, keep_ptr, out_ptr, n_partitions, n_out,
+                                             ids_ptr, kept_out_ptr, info_ptr, stream)
+        self.check(st, "dpg_compact_kept_async")
 
     def preaggregate(self, pid_ptr, pk_ptr, value_ptr, n, bound: BoundParams, pairs_ptr,
                      capacity, starts_ptr, stream) -> int:

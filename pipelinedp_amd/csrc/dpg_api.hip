@@ -1887,6 +1887,33 @@ int dpg_compact_kept(dpg_ctx *ctx, const uint8_t *keep, const double *out, int64
     return DPG_OK;
 }
 
+int dpg_compact_kept_async(dpg_ctx *ctx, const uint8_t *keep, const double *out, int64_t P,
+                           int32_t n_out, int64_t *kept_ids, double *kept_out, int64_t *info,
+                           void *stream) {
+    if (!ctx) return DPG_ERR_INVALID_ARG;
+    if (!keep || !kept_ids || !info || (n_out > 0 && (!out || !kept_out)))
+        return fail(ctx, DPG_ERR_INVALID_ARG, "null argument");
+    (void)hipSetDevice(ctx->device);
+    hipStream_t s = (hipStream_t)stream;
+    int st = DPG_OK;
+    HIP_TRY(hipMemsetAsync(info, 0, 16, s));
+    if (P > 0) {
+        uint32_t nb = (uint32_t)((P + kCompactPerBlock - 1) / kCompactPerBlock);
+        WS(bc, uint32_t, "compact.blocks", nb);
+        k_compact_count<<<nb, kCompactThreads, 0, s>>>(keep, P, bc);
+        LAUNCH_CHECK();
+        k_compact_scan<<<1, 1024, 0, s>>>(bc, nb, info);
+        LAUNCH_CHECK();
+        k_compact_write<<<nb, kCompactThreads, 0, s>>>(keep, out, P, n_out, bc, kept_ids, kept_out);
+        LAUNCH_CHECK();
+    }
+    // the error word as it stands now in stream order (the next bounding on
+    // this context reuses it)
+    if (ctx->last_err)
+        HIP_TRY(hipMemcpyAsync(info + 1, ctx->last_err, 4, hipMemcpyDeviceToDevice, s));
+    return DPG_OK;
+}
+
 int dpg_utility_analysis(dpg_ctx *ctx, const dpg_pair_entry *pairs,
                          const int64_t *partition_start, int64_t P, const dpg_ua_params *u,
                          double *raw, double *errors, double *keep, double *report,

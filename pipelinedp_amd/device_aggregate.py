@@ -10,10 +10,11 @@ Device pipeline per call (include/dpg.h):
   dpg_bound_aggregate -> [multi-GPU: reduce-scatter of the dense partials,
   or a fixed-block all-to-all of the occupied ones, with every rank's error
   flag: distributed.exchange_partials] -> dpg_select_and_noise ->
-  dpg_compact_kept (the one host synchronisation after the bounding).
+  dpg_compact_kept_async.  The kept count reaches the host when the result's
+  ids or values are first read (the one host synchronisation after the
+  bounding), so a caller can enqueue the next release first.
 """
 import ctypes
-import dataclasses
 import os
 from typing import Optional, Sequence
 
@@ -27,19 +28,59 @@ from pipelinedp_amd import distributed
 from pipelinedp_amd import partition_selection
 
 
+# experiments: DPG_SYNC_COMPACT=1 synchronises at the compaction, as before
+# round 5 (same-box A/B of the asynchronous result)
+_SYNC_COMPACT = os.environ.get("DPG_SYNC_COMPACT", "0") == "1"
+
+
 def _ptr(t: Optional[torch.Tensor]):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
 
-@dataclasses.dataclass
 class DeviceResult:
-    """Materialised result: kept partition ids and their metric columns, on the
-    device.  `keys()` maps ids back to the user's partition keys."""
-    partition_ids: torch.Tensor        # int64 [K] (global dense ids)
-    values: torch.Tensor               # float64 [K, len(fields)]
-    fields: tuple
-    key_table: Optional[Sequence]
-    stage_ms: dict = dataclasses.field(default_factory=dict)
+    """Materialised result: kept partition ids (int64 [K], global dense ids)
+    and their metric columns (float64 [K, len(fields)]), on the device.
+    `keys()` maps ids back to the user's partition keys.
+
+    Built from the compaction's full-size outputs and its device info word
+    (kept count, bounding error bits): the count is read -- and an internal
+    bounding error raised -- when `partition_ids` or `values` is first used."""
+
+    def __init__(self, partition_ids: torch.Tensor, values: torch.Tensor, fields: tuple,
+                 key_table: Optional[Sequence], stage_ms: Optional[dict] = None,
+                 pending: Optional[tuple] = None):
+        self._ids, self._vals = partition_ids, values
+        self.fields = fields
+        self.key_table = key_table
+        self.stage_ms = stage_ms if stage_ms is not None else {}
+        # (info int64[2] on the device, outputs per row, id stride, id offset)
+        self._pending = pending
+
+    def _resolve(self):
+        if self._pending is None:
+            return
+        info, n_out, stride, offset = self._pending
+        k, err = (int(x) for x in info.tolist())
+        if err & 2:
+            raise _native.NativeError(
+                "dpg_compact_kept failed (HIP error): internal hash-table error in bounding")
+        ids = self._ids[:k]
+        if stride != 1 or offset:  # several ranks: this rank's slice
+            ids = ids * stride + offset
+        self._ids = ids
+        self._vals = (self._vals[:k * n_out].view(k, n_out) if n_out
+                      else torch.empty((k, 0), dtype=torch.float64, device=self._vals.device))
+        self._pending = None
+
+    @property
+    def partition_ids(self) -> torch.Tensor:
+        self._resolve()
+        return self._ids
+
+    @property
+    def values(self) -> torch.Tensor:
+        self._resolve()
+        return self._vals
 
     def keys(self) -> list:
         return columnar.decode_keys(self.partition_ids.cpu().numpy(), self.key_table)
@@ -245,13 +286,19 @@ class DeviceAggregation:
             ctx.select_and_noise(lp, sel, nz, keep.data_ptr(), out.data_ptr(), sptr)
             ids = torch.empty(local_P, dtype=torch.int64, device=dev)
             kept_out = torch.empty(max(local_P * n_out, 1), **f64)
-            k = ctx.compact(keep.data_ptr(), out.data_ptr(), local_P, n_out, ids.data_ptr(),
-                            kept_out.data_ptr(), sptr)
-            ids = ids[:k]
-            if pk_stride != 1 or pk_offset:  # several ranks: this rank's slice
-                ids = ids * pk_stride + pk_offset
-            vals = kept_out[:k * n_out].view(k, n_out) if n_out else torch.empty((k, 0), **f64)
+            fields = self.plan.fields if self.plan is not None else ()
+            if _SYNC_COMPACT:  # A/B switch: the synchronising compaction
+                k = ctx.compact(keep.data_ptr(), out.data_ptr(), local_P, n_out,
+                                ids.data_ptr(), kept_out.data_ptr(), sptr)
+                info = torch.tensor([k, 0], dtype=torch.int64, device=dev)
+            else:
+                info = torch.empty(2, dtype=torch.int64, device=dev)
+                ctx.compact_async(keep.data_ptr(), out.data_ptr(), local_P, n_out,
+                                  ids.data_ptr(), kept_out.data_ptr(), info.data_ptr(), sptr)
+            res = DeviceResult(ids, kept_out, fields, enc.key_table, stage_ms,
+                               pending=(info, n_out, pk_stride, pk_offset))
             if backend.world_size > 1 and gather:
-                ids, vals = distributed.all_gather_results(ids, vals, backend.process_group)
-        fields = self.plan.fields if self.plan is not None else ()
-        return DeviceResult(ids, vals, fields, enc.key_table, stage_ms)
+                ids, vals = distributed.all_gather_results(res.partition_ids, res.values,
+                                                           backend.process_group)
+                res = DeviceResult(ids, vals, fields, enc.key_table, stage_ms)
+        return res

@@ -152,3 +152,49 @@ def test_error_flag_travels_and_fails_compaction(built):
     ctx.unpack_partials(part.data_ptr(), P, 1, 0, sl, stream)
     with pytest.raises(_native.NativeError, match="internal"):
         ctx.compact(keep.data_ptr(), None, 8, 0, ids.data_ptr(), None, stream)
+
+
+def test_async_compaction_matches_and_latches_error(built):
+    """dpg_compact_kept_async: the same ids and rows as the synchronising
+    compaction, the count and the bounding's error bits in a device word;
+    DeviceResult reads them on first use and raises the internal error
+    there (what the synchronising call raises at once)."""
+    from pipelinedp_amd import _native
+    from pipelinedp_amd.device_aggregate import DeviceResult
+    backend, parts, P = _aggregate()
+    ctx = backend.ctx
+    dev = parts["rows"].device
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    g = torch.Generator(device="cpu").manual_seed(7)
+    n, n_out = 5000, 3
+    keep = (torch.rand(n, generator=g) < 0.3).to(torch.uint8).to(dev)
+    out = torch.randn(n * n_out, generator=g, dtype=torch.float64).to(dev)
+    ids_s = torch.empty(n, dtype=torch.int64, device=dev)
+    vals_s = torch.empty(n * n_out, dtype=torch.float64, device=dev)
+    k = ctx.compact(keep.data_ptr(), out.data_ptr(), n, n_out, ids_s.data_ptr(),
+                    vals_s.data_ptr(), stream)
+    ids_a = torch.empty(n, dtype=torch.int64, device=dev)
+    vals_a = torch.empty(n * n_out, dtype=torch.float64, device=dev)
+    info = torch.full((2,), -1, dtype=torch.int64, device=dev)
+    ctx.compact_async(keep.data_ptr(), out.data_ptr(), n, n_out, ids_a.data_ptr(),
+                      vals_a.data_ptr(), info.data_ptr(), stream)
+    res = DeviceResult(ids_a, vals_a, ("a", "b", "c"), None, pending=(info, n_out, 1, 0))
+    assert k == int(keep.sum())
+    assert torch.equal(res.partition_ids, ids_s[:k])
+    assert torch.equal(res.values, vals_s[:k * n_out].view(k, n_out))
+    assert torch.equal(res.partition_ids, torch.nonzero(keep).flatten())
+    # a latched internal error (as an exchanged block carries it) is raised
+    # when the result is first read
+    names = [k for k in ("rows", "count", "sum") if parts.get(k) is not None]
+    part = torch.zeros(len(names) * P + 1, dtype=torch.float64, device=dev)
+    part[-1] = 1.0
+    tgt = {k: torch.empty(P, dtype=parts[k].dtype, device=dev) for k in names}
+    sl = _native.Partials(P, *(tgt[k].data_ptr() if k in tgt else None
+                               for k in ("rows", "count", "sum", "nsum", "nsq")))
+    ctx.unpack_partials(part.data_ptr(), P, 1, 0, sl, stream)
+    info2 = torch.empty(2, dtype=torch.int64, device=dev)
+    ctx.compact_async(keep.data_ptr(), out.data_ptr(), n, n_out, ids_a.data_ptr(),
+                      vals_a.data_ptr(), info2.data_ptr(), stream)
+    bad = DeviceResult(ids_a, vals_a, ("a", "b", "c"), None, pending=(info2, n_out, 1, 0))
+    with pytest.raises(_native.NativeError, match="internal"):
+        bad.partition_ids
