@@ -2032,10 +2032,21 @@ int dpg_utility_analysis(dpg_ctx *ctx, const dpg_pair_entry *pairs,
     a.err = errors;
     a.mom = mom;
     a.keep = keep;
-    HIP_TRY(hipMemsetAsync(raw, 0, (size_t)P * 2 * 8, s));
-    HIP_TRY(hipMemsetAsync(errors, 0, (size_t)P * a.n_metrics * 5 * C * 8, s));
-    HIP_TRY(hipMemsetAsync(mom, 0, (size_t)P * kUaMom * C * 8, s));
-    if (keep) HIP_TRY(hipMemsetAsync(keep, 0, (size_t)P * C * 8, s));
+    // public partitions: every public row is added to (k_ua_public), so all
+    // start from zero; private: only the rows of partitions split between
+    // accumulate runs (k_ua_zero_split; DPG_UA_FULL_ZERO=1: the full fill,
+    // for A/B runs)
+    static const bool full_zero = std::getenv("DPG_UA_FULL_ZERO") != nullptr;
+    if (u->public_partitions || full_zero) {
+        HIP_TRY(hipMemsetAsync(raw, 0, (size_t)P * 2 * 8, s));
+        HIP_TRY(hipMemsetAsync(errors, 0, (size_t)P * a.n_metrics * 5 * C * 8, s));
+        HIP_TRY(hipMemsetAsync(mom, 0, (size_t)P * kUaMom * C * 8, s));
+        if (keep) HIP_TRY(hipMemsetAsync(keep, 0, (size_t)P * C * 8, s));
+    } else {
+        const unsigned g = (unsigned)std::min<int64_t>((P + 3) / 4, (int64_t)ctx->n_cu * 8);
+        k_ua_zero_split<<<g, 256, 0, s>>>(partition_start, a);
+        LAUNCH_CHECK();
+    }
     int64_t n = 0;
     HIP_TRY(hipMemcpyAsync(&n, partition_start + P, 8, hipMemcpyDeviceToHost, s));
     if (n_out) *n_out = 0;

@@ -294,6 +294,29 @@ __global__ __launch_bounds__(64) void k_ua_accumulate(const ItemPA *pairs,
     flush(cur);
 }
 
+// Private partitions: the rows k_ua_accumulate adds atomically -- those of
+// partitions split between runs of kUaRun pairs -- start from zero.  Every
+// other row of a partition with pairs is written by plain stores, and rows
+// of partitions without pairs are never read (the output is the partitions
+// with pairs), so the ~9.7 GB of per-partition outputs of a 64-configuration
+// sweep over 1e6 partitions need no zero fill.  One wave per partition;
+// vector stores only.
+__global__ __launch_bounds__(256) void k_ua_zero_split(const int64_t *pstart, UaArgs a) {
+    const int lane = (int)__lane_id();
+    const int64_t C64 = a.n_configs;
+    const int64_t E = (int64_t)a.n_metrics * 5 * C64;  // error row
+    const int64_t M = (int64_t)kUaMom * C64;            // moments row
+    const int64_t w0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t k = w0; k < a.P; k += nw) {
+        const int64_t b = pstart[k], e = pstart[k + 1];  // wave-uniform
+        if (e <= b || b / kUaRun == (e - 1) / kUaRun) continue;
+        if (lane < 2) a.raw[2 * k + lane] = 0.0;
+        for (int64_t i = lane; i < E; i += 64) a.err[k * E + i] = 0.0;
+        for (int64_t i = lane; i < M; i += 64) a.mom[k * M + i] = 0.0;
+    }
+}
+
 // The empty accumulator every public partition carries (count 0, sum 0, 0
 // partitions): one more privacy id in the raw statistics, and the SUM
 // clipping of a zero contribution.  Runs after k_ua_accumulate.
