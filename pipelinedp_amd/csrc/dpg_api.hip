@@ -381,7 +381,7 @@ int run_level_grouped(dpg_ctx *ctx, hipStream_t s, const Src &src, uint32_t S,
         k_build_tiles_single<<<(ng + 255) / 256, 256, 0, s>>>(n_upper, gsz, 1u, groups, stb, snt,
                                                              ngrp, XcdQueues{});
     } else {
-        k_build_tiles<<<(S + 255) / 256, 256, 0, s>>>(seg_start, seg_cnt, seg_cnt64, S, gsz,
+        k_build_tiles<<<build_tiles_blocks(S), 256, 0, s>>>(seg_start, seg_cnt, seg_cnt64, S, gsz,
                                                       groups, stb, snt, ngrp, XcdQueues{});
     }
     LAUNCH_CHECK();
@@ -474,7 +474,7 @@ int run_level(dpg_ctx *ctx, hipStream_t s, const Src &src, uint32_t S, const int
                                                              (uint32_t)(DPG_L1_GROUP * ctx->n_cu / 8),
                                                              tiles, stb, snt, ntiles_dev, xq);
     } else {
-        k_build_tiles<<<(S + 255) / 256, 256, 0, s>>>(seg_start, seg_cnt, seg_cnt64, S, tile, tiles,
+        k_build_tiles<<<build_tiles_blocks(S), 256, 0, s>>>(seg_start, seg_cnt, seg_cnt64, S, tile, tiles,
                                                       stb, snt, ntiles_dev, xq);
     }
     LAUNCH_CHECK();
@@ -1080,7 +1080,7 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
         WS(rt, TileDesc, "reduce.tiles", max_tiles);
         WS(rstb, uint32_t, "reduce.stb", F);
         WS(rsnt, uint32_t, "reduce.snt", F);
-        k_build_tiles<<<(F + 255) / 256, 256, 0, s>>>(baseR, totR, nullptr, F, rtile, rt, rstb,
+        k_build_tiles<<<build_tiles_blocks(F), 256, 0, s>>>(baseR, totR, nullptr, F, rtile, rt, rstb,
                                                       rsnt, &ctl->ntiles[5]);
         LAUNCH_CHECK();
         size_t lds_r = (size_t)kRange * 8 * (ItemTraits<Item>::var ? (ItemTraits<Item>::sum ? 3 : 2) : 1) +

@@ -403,32 +403,48 @@ __global__ void k_build_subtiles(const TileDesc *groups, const uint32_t *ngroups
     for (uint32_t j = 0; j < nt; ++j) xq.q[(size_t)x * xq.stride + qb + j] = b + j;
 }
 
-__global__ void k_build_tiles(const int64_t *seg_start, const uint32_t *seg_cnt,
-                              const int64_t *seg_cnt64, uint32_t S, int64_t tile,
-                              TileDesc *tiles, uint32_t *seg_tile_base, uint32_t *seg_ntiles,
-                              uint32_t *ntiles_total, XcdQueues xq = XcdQueues{}) {
-    uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= S) return;
-    int64_t st = seg_start ? seg_start[s] : 0;
-    int64_t n = seg_cnt64 ? seg_cnt64[s] : (int64_t)seg_cnt[s];
-    uint32_t nt = (uint32_t)((n + tile - 1) / tile);
-    uint32_t b = nt ? atomicAdd(ntiles_total, nt) : 0;
-    seg_tile_base[s] = b;
-    seg_ntiles[s] = nt;
-    for (uint32_t j = 0; j < nt; ++j) {
+// One wave per segment (launch build_tiles_blocks(S) blocks of 256): lane 0
+// reserves the segment's tile range, the lanes write its tiles.  (One thread
+// per segment left a single segment of thousands of tiles -- the item level
+// -- to one thread's serial loop: 92 us per release at config 2.)
+__global__ __launch_bounds__(256) void k_build_tiles(const int64_t *seg_start,
+                                                     const uint32_t *seg_cnt,
+                                                     const int64_t *seg_cnt64, uint32_t S,
+                                                     int64_t tile, TileDesc *tiles,
+                                                     uint32_t *seg_tile_base,
+                                                     uint32_t *seg_ntiles,
+                                                     uint32_t *ntiles_total,
+                                                     XcdQueues xq = XcdQueues{}) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t s = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (s >= S) return;  // wave-uniform
+    const int64_t st = seg_start ? seg_start[s] : 0;
+    const int64_t n = seg_cnt64 ? seg_cnt64[s] : (int64_t)seg_cnt[s];
+    const uint32_t nt = (uint32_t)((n + tile - 1) / tile);
+    const uint32_t x = s & 7u;
+    uint32_t b = 0, qb = 0;
+    if (lane == 0 && nt) {
+        b = atomicAdd(ntiles_total, nt);
+        if (xq.q) qb = atomicAdd(&xq.n[x], nt);
+    }
+    b = (uint32_t)__shfl((int)b, 0, 64);
+    qb = (uint32_t)__shfl((int)qb, 0, 64);
+    if (lane == 0) {
+        seg_tile_base[s] = b;
+        seg_ntiles[s] = nt;
+    }
+    for (uint32_t j = lane; j < nt; j += 64) {
         TileDesc d;
         d.begin = st + (int64_t)j * tile;
         d.end = st + min((int64_t)(j + 1) * tile, n);
         d.seg = s;
         d.pad = 0;
         tiles[b + j] = d;
-    }
-    if (xq.q && nt) {
-        const uint32_t x = s & 7u;
-        const uint32_t qb = atomicAdd(&xq.n[x], nt);
-        for (uint32_t j = 0; j < nt; ++j) xq.q[(size_t)x * xq.stride + qb + j] = b + j;
+        if (xq.q) xq.q[(size_t)x * xq.stride + qb + j] = b + j;
     }
 }
+
+inline uint32_t build_tiles_blocks(uint32_t S) { return (S + 3) / 4; }
 
 // ---------------------------------------------------------------- hist
 template <class Src>
