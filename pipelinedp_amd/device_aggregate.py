@@ -53,13 +53,18 @@ class DeviceResult:
         self.fields = fields
         self.key_table = key_table
         self.stage_ms = stage_ms if stage_ms is not None else {}
-        # (info int64[2] on the device, outputs per row, id stride, id offset)
+        # (info int64[2] on the device, outputs per row, id stride, id offset
+        # [, event recorded behind the compaction on the release's stream])
         self._pending = pending
 
     def _resolve(self):
         if self._pending is None:
             return
-        info, n_out, stride, offset = self._pending
+        info, n_out, stride, offset = self._pending[:4]
+        if len(self._pending) > 4 and self._pending[4] is not None:
+            # the release ran on the stream current at materialize(); the
+            # reader's current stream may be another one
+            self._pending[4].synchronize()
         k, err = (int(x) for x in info.tolist())
         if err & 2:
             raise _native.NativeError(
@@ -295,8 +300,10 @@ class DeviceAggregation:
                 info = torch.empty(2, dtype=torch.int64, device=dev)
                 ctx.compact_async(keep.data_ptr(), out.data_ptr(), local_P, n_out,
                                   ids.data_ptr(), kept_out.data_ptr(), info.data_ptr(), sptr)
+            done = torch.cuda.Event()
+            done.record(stream)
             res = DeviceResult(ids, kept_out, fields, enc.key_table, stage_ms,
-                               pending=(info, n_out, pk_stride, pk_offset))
+                               pending=(info, n_out, pk_stride, pk_offset, done))
             if backend.world_size > 1 and gather:
                 ids, vals = distributed.all_gather_results(res.partition_ids, res.values,
                                                            backend.process_group)
