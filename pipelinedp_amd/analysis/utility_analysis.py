@@ -282,21 +282,19 @@ class UtilityAnalysis:
         field layout of dpg_utility_analysis' report output, as a list of
         Python floats: per-element numpy scalar access dominated the report
         assembly of a 64-configuration sweep)."""
+        # positional construction throughout (fields in declaration order,
+        # metrics.py): keyword matching was half of the assembly time of a
+        # 64-configuration report set
         public = self.public is not None
         if public:
-            info = metrics.PartitionsInfo(public_partitions=True,
-                                          num_dataset_partitions=int(round(v[2])),
-                                          num_non_public_partitions=0,
-                                          num_empty_partitions=int(round(v[3])))
+            info = metrics.PartitionsInfo(True, int(round(v[2])), 0, int(round(v[3])))
         else:
             # the reference sets strategies[configuration_index] while the
             # index is still -1 (utility_analysis.py:117-129 runs before
             # :218-229 assigns it): every report names the LAST strategy
-            info = metrics.PartitionsInfo(public_partitions=False,
-                                          num_dataset_partitions=int(round(v[0])),
-                                          strategy=self.strategies[-1],
-                                          kept_partitions=metrics.MeanVariance(v[2], v[3]))
-        report = metrics.UtilityReport(configuration_index=c, partitions_info=info)
+            info = metrics.PartitionsInfo(False, int(round(v[0])), None, None,
+                                          self.strategies[-1], metrics.MeanVariance(v[2], v[3]))
+        report = metrics.UtilityReport(c, info)
         if not self.metrics:
             return report
         total_w = v[1]
@@ -305,14 +303,13 @@ class UtilityAnalysis:
         cf = self.configs[c]
         noise_kind = cf.params.noise_kind
 
-        def verr(x):
-            return metrics.ValueErrors(
-                bounding_errors=metrics.ContributionBoundingErrors(
-                    l0=metrics.MeanVariance(mean=x[0] * wscale, var=x[1] * wscale),
-                    linf_min=x[2] * wscale, linf_max=x[3] * wscale),
-                mean=x[4] * wscale, variance=x[5] * wscale, rmse=x[6] * wscale,
-                l1=x[7] * wscale, rmse_with_dropped_partitions=x[8] * wscale,
-                l1_with_dropped_partitions=x[9] * wscale)
+        VE, CBE, MV = metrics.ValueErrors, metrics.ContributionBoundingErrors, metrics.MeanVariance
+
+        def verr(b):  # ValueErrors from the 10 weighted sums at v[b:b + 10]
+            w = wscale
+            return VE(CBE(MV(v[b] * w, v[b + 1] * w), v[b + 2] * w, v[b + 3] * w),
+                      v[b + 4] * w, v[b + 5] * w, v[b + 6] * w, v[b + 7] * w, v[b + 8] * w,
+                      v[b + 9] * w)
         # the reference labels metric_errors by zipping them with the user's
         # metric order (cross_partition_combiners.py:208-212)
         for mi, (m, um, std) in enumerate(zip(self.metrics, self._user_metrics, cf.std_list)):
@@ -320,11 +317,9 @@ class UtilityAnalysis:
             tot = v[b]
             dscale = 1.0 if tot == 0 else 1.0 / tot
             errs.append(metrics.MetricUtility(
-                metric=um, noise_std=std, noise_kind=noise_kind,
-                ratio_data_dropped=metrics.DataDropInfo(l0=v[b + 1] * dscale,
-                                                        linf=v[b + 2] * dscale,
-                                                        partition_selection=v[b + 3] * dscale),
-                absolute_error=verr(v[b + 4:b + 14]), relative_error=verr(v[b + 14:b + 24])))
+                um, std, noise_kind,
+                metrics.DataDropInfo(v[b + 1] * dscale, v[b + 2] * dscale, v[b + 3] * dscale),
+                verr(b + 4), verr(b + 14)))
         report.metric_errors = errs
         return report
 
