@@ -1992,7 +1992,7 @@ int dpg_utility_analysis(dpg_ctx *ctx, const dpg_pair_entry *pairs,
     }
     a.n_cls = (int32_t)cls_rep.size();
     // pi(0 .. npi - 1) per class in LDS: at least the exact PMF's 104
-    // counts, at most 32 KB, and no further than the last count whose keep
+    // counts, at most 16 KB, and no further than the last count whose keep
     // probability is below 1 (ua_pi_range; beyond it the normal
     // approximation telescopes without reading pi): the smaller the table,
     // the more waves of k_ua_select share a CU
@@ -2009,8 +2009,11 @@ int dpg_utility_analysis(dpg_ctx *ctx, const dpg_pair_entry *pairs,
             i1 = (int64_t)std::ceil(r.threshold + 8.5 * r.scale) + sh;
         top = std::max(top, i1 + 1);
     }
+    // (16 KB: the normal-approximation pass is latency-bound, and a table of
+    // 32 KB held it at 5 waves per CU; counts past the table read pi from
+    // the keep table in global memory)
     a.npi = (int32_t)std::max<int64_t>(
-        kPgfB * kPgfNB, std::min<int64_t>(top, (32 * 1024 / 8) / a.n_cls));
+        kPgfB * kPgfNB, std::min<int64_t>(top, (16 * 1024 / 8) / a.n_cls));
     WS(dcls, int32_t, "ua.cls", C + cls_rep.size());
     std::vector<int32_t> hcls(cls);
     hcls.insert(hcls.end(), cls_rep.begin(), cls_rep.end());

@@ -507,11 +507,21 @@ __global__ __launch_bounds__(64) void k_ua_select(const ItemPA *pairs, const int
             // instead of once per configuration lane; counts with 0 < pi < 1
             // are evaluated one by one (below i0 pi is 0, above i1 it is 1
             // and the remaining mass telescopes to G(en) - G(i1)).
+            // the moments of every class in one round of loads, lane kc
+            // holding class kc's (one dependent load round per class before:
+            // the pass is latency-bound, one partition per wave)
+            double m0 = 0.0, m1 = 0.0, m2 = 0.0;
+            if (c < K) {
+                const double *mm = a.mom + k * kUaMom * C64 + a.cls_rep[c];
+                m0 = mm[0];
+                m1 = mm[C64];
+                m2 = mm[2 * C64];
+            }
             for (int kc = 0; kc < K; ++kc) {
                 const int rc = a.cls_rep[kc];
                 const UaConfig cr = a.cfg[rc];
-                const double *mm = a.mom + k * kUaMom * C64 + rc;
-                const double mean = mm[0], sd = sqrt(mm[C64]);
+                const double mean = __shfl(m0, kc, 64), sd = sqrt(__shfl(m1, kc, 64));
+                const double m2k = __shfl(m2, kc, 64);
                 double kp;
                 auto pi_k = [&](int64_t i) {
                     return i < NPI ? spi[i * K + kc] : ua_pi(cr, a.tables, i);
@@ -519,7 +529,7 @@ __global__ __launch_bounds__(64) void k_ua_select(const ItemPA *pairs, const int
                 if (sd == 0.0) {
                     kp = pi_k((int64_t)rint(mean));
                 } else {
-                    const double skew = mm[2 * C64] / (sd * sd * sd);
+                    const double skew = m2k / (sd * sd * sd);
                     const int64_t st = (int64_t)fmax(0.0, floor(mean - 8.0 * sd));
                     const int64_t en = (int64_t)fmin((double)n, rint(mean + 8.0 * sd));
                     auto Gc = [&](int64_t i) {
