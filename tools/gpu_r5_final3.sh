@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round-5 closing evidence: tools/gpu_r5_final.sh (GPU suite, smoke, bench
+# lines, host split, rocprofv3 kernel stats, PMC traffic, phase clocks),
+# then a same-box config-5 A/B of the block-aggregated order kernel against
+# the previous build (libdpg_prev.so).
+set -o pipefail
+export TMPDIR=/tmp
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd $R
+TAG=${TAG:-r5final3} bash tools/gpu_r5_final.sh || exit 1
+TAG=${TAG:-r5final3}/ab STEPS=3 BENCH_ARGS="--workload config5" VARIANTS="new:DPG_X=0 prev:DPG_LIB_PATH=pipelinedp_amd/lib/libdpg_prev.so" bash tools/gpu_env_ab.sh
