@@ -2130,7 +2130,9 @@ int dpg_utility_analysis(dpg_ctx *ctx, const dpg_pair_entry *pairs,
         uint32_t run = 0, start[kUaBuckets];
         for (int b = 0; b < kUaBuckets; ++b) start[b] = run, run += hc[b];
         UPLOAD(bcount, start, sizeof(start));
-        k_ua_order<<<gb, 256, 0, s>>>(a);
+        const unsigned go = (unsigned)std::min<int64_t>((P + 256 * kUaOrderPer - 1) / (256 * kUaOrderPer),
+                                                       (int64_t)ctx->n_cu * 8);
+        k_ua_order<<<go, 256, 0, s>>>(a);
         LAUNCH_CHECK();
         if (run > 0) {
             k_ua_report<<<(unsigned)((run + kUaRepRun - 1) / kUaRepRun), 64, 0, s>>>((int64_t)run, a);

@@ -609,24 +609,34 @@ __global__ __launch_bounds__(256) void k_ua_bucket(const int64_t *pstart, UaArgs
 
 // bcount holds each bucket's start: every output partition takes a slot of
 // its bucket (one atomic per distinct bucket of a wave)
+// Output partitions grouped by size bucket (k_ua_report sums each bucket's
+// partitions): per block of kUaOrderPer x 256 partitions, bucket counts in
+// LDS, one reservation per bucket per block, then the partitions written at
+// their LDS-local offsets.  (One reservation per bucket per wave made ~16K
+// waves contend for the few hot bucket counters: 1.2 ms at config 5.)
+constexpr int kUaOrderPer = 8;
 __global__ __launch_bounds__(256) void k_ua_order(UaArgs a) {
-    const uint32_t lane = __lane_id();
-    for (int64_t k0 = (int64_t)blockIdx.x * blockDim.x; k0 < a.P;
-         k0 += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t k = k0 + threadIdx.x;
-        const int b = k < a.P ? a.bucket[k] : -1;
-        uint64_t todo = __ballot(b >= 0);
-        while (todo) {
-            const int l = __builtin_ctzll(todo);
-            const int bb = __builtin_amdgcn_readlane(b, l);
-            const uint64_t same = __ballot(b == bb) & todo;
-            uint32_t base = 0;
-            if ((int)lane == l) base = atomicAdd(&a.bcount[bb], (uint32_t)__popcll(same));
-            base = __builtin_amdgcn_readlane(base, l);
-            if ((same >> lane) & 1ull)
-                a.order[base + __popcll(same & ((1ull << lane) - 1ull))] = k;
-            todo &= ~same;
+    __shared__ uint32_t cnt[kUaBuckets], base[kUaBuckets];
+    const int64_t step = (int64_t)blockDim.x * kUaOrderPer;
+    for (int64_t k0 = (int64_t)blockIdx.x * step; k0 < a.P; k0 += (int64_t)gridDim.x * step) {
+        if (threadIdx.x < kUaBuckets) cnt[threadIdx.x] = 0;
+        __syncthreads();
+        int bk[kUaOrderPer];
+        uint32_t rk[kUaOrderPer];
+#pragma unroll
+        for (int u = 0; u < kUaOrderPer; ++u) {
+            const int64_t k = k0 + (int64_t)u * blockDim.x + threadIdx.x;
+            bk[u] = k < a.P ? a.bucket[k] : -1;
+            rk[u] = bk[u] >= 0 ? atomicAdd(&cnt[bk[u]], 1u) : 0u;
         }
+        __syncthreads();
+        if (threadIdx.x < kUaBuckets && cnt[threadIdx.x])
+            base[threadIdx.x] = atomicAdd(&a.bcount[threadIdx.x], cnt[threadIdx.x]);
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < kUaOrderPer; ++u)
+            if (bk[u] >= 0) a.order[base[bk[u]] + rk[u]] = k0 + (int64_t)u * blockDim.x + threadIdx.x;
+        __syncthreads();  // cnt / base are rewritten by the next round
     }
 }
 
