@@ -226,3 +226,50 @@ def test_preaggregate_value_records_match_gather_path(built, exact, monkeypatch)
         np.testing.assert_array_equal(got["sum"], want["sum"])
     else:
         np.testing.assert_allclose(got["sum"], want["sum"], rtol=1e-12, atol=1e-9)
+
+
+def test_64_config_sweep_with_partition_sampling_matches_oracle(built):
+    """The 64-configuration sweep with partitions_sampling_prob = 0.5:
+    sampled-out partitions are skipped by the accumulate (their rows are
+    neither written nor, being outside the output, read -- including rows
+    of partitions split between accumulate runs, which the sweep zeroes
+    without a full fill), by the selection and by the report; per-partition
+    values and reports equal the oracle's on the sampled set within 1e-7."""
+    from pipelinedp_amd.analysis import utility_analysis as ua_mod
+    rng = np.random.default_rng(56)
+    n, n_pid, P = 200_000, 4_000, 300
+    pid = rng.integers(0, n_pid, n)
+    w = np.arange(1, P + 1, dtype=np.float64) ** -1.1
+    pk = rng.choice(P, size=n, p=w / w.sum())
+    val = rng.uniform(-1, 6, n)
+    mpc, mcpp = _grid_configs(8)
+    multi = analysis.MultiParameterConfiguration(
+        max_partitions_contributed=mpc, max_contributions_per_partition=mcpp,
+        min_sum_per_partition=[0.0] * 64, max_sum_per_partition=[float(b) for b in mcpp])
+    params = pdp.AggregateParams(noise_kind=pdp.NoiseKind.LAPLACE,
+                                 metrics=[pdp.Metrics.COUNT, pdp.Metrics.SUM,
+                                          pdp.Metrics.PRIVACY_ID_COUNT],
+                                 max_partitions_contributed=1, max_contributions_per_partition=1,
+                                 min_sum_per_partition=0.0, max_sum_per_partition=1.0)
+    prob = 0.5
+    opts = analysis.UtilityAnalysisOptions(epsilon=1.0, delta=1e-6, aggregate_params=params,
+                                           multi_param_configuration=multi,
+                                           partitions_sampling_prob=prob)
+    cols = pdp.ColumnarData(pid=torch.as_tensor(pid), pk=torch.as_tensor(pk),
+                            value=torch.as_tensor(val), n_partitions=P)
+    reports, per = _run(cols, opts, pdp.DataExtractors("pid", "pk", "value"))
+    bound = ua_mod._sample_bound(prob)
+    keep = lambda k: ua_mod._keep_by_hash(k, bound)
+    cfgs = [dict(mpc=a, mcpp=b, min_sum=0.0, max_sum=float(b), noise_kind="LAPLACE",
+                 strategy="TRUNCATED_GEOMETRIC", pre_threshold=None) for a, b in zip(mpc, mcpp)]
+    pairs = uo.preaggregate(pid.tolist(), pk.tolist(), val.tolist(), None)
+    # partitions split between runs of 1024 pairs, sampled in and out
+    assert sum(len(v) > 1024 for k, v in pairs.items() if keep(k)) > 0
+    assert sum(len(v) > 1024 for k, v in pairs.items() if not keep(k)) > 0
+    want_per, want_rep = uo.analyze(pairs, cfgs, ["COUNT", "SUM", "PRIVACY_ID_COUNT"], 1.0, 1e-6,
+                                    "LAPLACE", sampled=keep)
+    assert set(per) == set(want_per) and len(want_per) > 0
+    for key, want in want_per.items():
+        uc.assert_close(want, per[key], f"per{key}", atol=1e-7, rtol=1e-7)
+    for want, got in zip(want_rep, reports):
+        uc.assert_close(want, got, "report", atol=1e-7, rtol=1e-7)
