@@ -726,12 +726,12 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     // chunks, so two waves sharing a SIMD next to SIMDs with one would finish
     // last (same-box A/B, config 4 with 32-KB working sets: 5 waves per CU
     // 42 ms, 4 per CU 29.7 ms)
-    auto waves_per_cu = [&](const void *kern, size_t lds) {
+    auto waves_per_cu = [&](const void *kern, size_t lds, int cap = 16) {
         int wpc = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&wpc, kern, 64, lds) != hipSuccess ||
             wpc <= 0)
             wpc = 1;
-        int pc = std::min(wpc, (int)std::min<size_t>(16, (160 * 1024) / lds));
+        int pc = std::min(wpc, (int)std::min<size_t>((size_t)cap, (160 * 1024) / lds));
         if (pc > 4) pc &= ~3;
         if (const char *e = std::getenv("DPG_DEBUG_WPC"))  // debug: occupancy experiments
             pc = std::max(1, std::min(pc, std::atoi(e)));
@@ -748,22 +748,31 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
             b = 1;
         return b;
     };
-    const void *narrow = nullptr, *wide = nullptr;
+    const void *narrow = nullptr, *mid = nullptr, *wide = nullptr;
+    size_t mid_lds = wave_lds, wide_lds = wave_lds;
+    constexpr bool kMid = kHasMid<R>;
     if constexpr (!ItemTraits<Item>::preagg) {
         if (use_sort && !wpk) {
-            narrow = (const void *)k_bound_sorted<Item, R, false, false>;
-            wide = (const void *)k_bound_sorted<Item, R, true, false>;
-            wave_lds = SortLayout<Item, R, false>::TOTAL;
+            narrow = (const void *)k_bound_sorted<Item, R, 0, false>;
+            if constexpr (kMid) mid = (const void *)k_bound_sorted<Item, R, 1, false>;
+            wide = (const void *)k_bound_sorted<Item, R, 2, false>;
+            wave_lds = SortLayout<Item, R, false, kTierCand<R, 0>>::TOTAL;
+            mid_lds = SortLayout<Item, R, false, kTierCand<R, 1>>::TOTAL;
+            wide_lds = SortLayout<Item, R, false, kTierCand<R, 2>>::TOTAL;
         }
         if constexpr (sizeof(R) == 12) {
             if (use_sort && wpk) {
-                narrow = (const void *)k_bound_sorted<Item, R, false, true>;
-                wide = (const void *)k_bound_sorted<Item, R, true, true>;
-                wave_lds = SortLayout<Item, R, true>::TOTAL;
+                narrow = (const void *)k_bound_sorted<Item, R, 0, true>;
+                if constexpr (kMid) mid = (const void *)k_bound_sorted<Item, R, 1, true>;
+                wide = (const void *)k_bound_sorted<Item, R, 2, true>;
+                wave_lds = SortLayout<Item, R, true, kTierCand<R, 0>>::TOTAL;
+                mid_lds = SortLayout<Item, R, true, kTierCand<R, 1>>::TOTAL;
+                wide_lds = SortLayout<Item, R, true, kTierCand<R, 2>>::TOTAL;
             }
         }
     }
-    const int per_cu = waves_per_cu(use_sort ? narrow : (const void *)wave_kern, wave_lds);
+    const int per_cu = use_sort ? waves_per_cu(narrow, wave_lds, 4 * kNarrowWPS<R>)
+                                : waves_per_cu((const void *)wave_kern, wave_lds);
     const uint32_t Gw = (uint32_t)(ctx->n_cu * per_cu);
     const uint32_t Gm = hctl.n_mchunks ? (uint32_t)std::min<uint32_t>(
                                              ctx->n_cu * CL::PER_CU, hctl.n_mchunks)
@@ -804,18 +813,28 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     if constexpr (!ItemTraits<Item>::preagg) if (use_sort) {
         WS(defer, uint8_t, "bound.defer", std::max<size_t>(chunk_cap, 1));
         (void)hipFuncSetAttribute(narrow, hipFuncAttributeMaxDynamicSharedMemorySize, (int)wave_lds);
-        (void)hipFuncSetAttribute(wide, hipFuncAttributeMaxDynamicSharedMemorySize, (int)wave_lds);
+        if (mid) (void)hipFuncSetAttribute(mid, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mid_lds);
+        (void)hipFuncSetAttribute(wide, hipFuncAttributeMaxDynamicSharedMemorySize, (int)wide_lds);
         auto launch = [&](auto wpk_tag) {
             constexpr bool W = decltype(wpk_tag)::value;
-            k_bound_sorted<Item, R, false, W><<<Gw, 64, wave_lds, s>>>(
+            k_bound_sorted<Item, R, 0, W><<<Gw, 64, wave_lds, s>>>(
                 recs, refined, hrec, chunk_list, &ctl->n_chunks, bpl, items, wg_off, wg_cnt, defer,
                 Gw);
-            // chunks with more candidates than the narrow kernel sorts: two
-            // waves per chunk (4 waves per SIMD) or, DPG_MW_OFF, the
-            // single-wave 8-element kernel (2 waves per SIMD)
-            stage(ctx, s, "bound.wide");
             BoundParams bpx = bpl;
             bpx.phase_cyc = nullptr;
+            if constexpr (kMid) {
+                // chunks of 129-256 candidates: 4 waves per SIMD
+                stage(ctx, s, "bound.mid");
+                const uint32_t Gx = std::min<uint32_t>(
+                    Gw, (uint32_t)(ctx->n_cu * waves_per_cu(mid, mid_lds)));
+                k_bound_sorted<Item, R, 1, W><<<Gx, 64, mid_lds, s>>>(
+                    recs, refined, hrec, chunk_list, &ctl->n_chunks, bpx, items, wg_off, wg_cnt,
+                    defer, Gw);
+            }
+            // chunks with more candidates than the narrow / mid passes sort:
+            // two waves per chunk (4 waves per SIMD) or, DPG_MW_OFF, the
+            // single-wave 8-element kernel (2 waves per SIMD)
+            stage(ctx, s, "bound.wide");
             if (use_mw) {
                 if (timing) bpx.phase_cyc = bpl.phase_cyc + 48;
                 using LW = SortLayoutMW<Item, R, W, 2>;
@@ -829,8 +848,8 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
                     defer, Gw);
             } else {
                 const uint32_t Gx = std::min<uint32_t>(
-                    Gw, (uint32_t)(ctx->n_cu * waves_per_cu(wide, wave_lds)));
-                k_bound_sorted<Item, R, true, W><<<Gx, 64, wave_lds, s>>>(
+                    Gw, (uint32_t)(ctx->n_cu * waves_per_cu(wide, wide_lds)));
+                k_bound_sorted<Item, R, 2, W><<<Gx, 64, wide_lds, s>>>(
                     recs, refined, hrec, chunk_list, &ctl->n_chunks, bpx, items, wg_off, wg_cnt,
                     defer, Gw);
             }

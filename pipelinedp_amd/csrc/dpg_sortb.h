@@ -61,6 +61,9 @@ constexpr uint64_t kSkPad = ~0ull;  // padding elements (real keys have bit 63 c
 #define DPG_SORT_LATE 1  // value gathers of over-full pairs after their mcpp sample
 #endif
 constexpr bool kSortLate = DPG_SORT_LATE != 0;
+#ifndef DPG_SORT_PF
+#define DPG_SORT_PF 0  // 8-byte records: the narrow pass prefetches the next chunk (see kSortPF)
+#endif
 
 // The wave's LDS working set is kept under 10 KB (COUNT / SUM items) so that
 // 16 waves share a CU: the kernel is latency-bound per wave (same-box A/B,
@@ -70,9 +73,13 @@ constexpr bool kSortLate = DPG_SORT_LATE != 0;
 // pair starts are 16-bit, and the candidate area is reused: candidate keys
 // and indices -> record keys of over-full pairs (phase M) -> accumulators
 // per pair (phase F).
-template <class Item, class R, bool kWPk = false>
+// kC: candidates the working set holds -- kTierCand of the pass (kNarrowCand
+// for the narrow one (round 5: a smaller working set is what lets more waves
+// share a CU, see k_bound_sorted)
+template <class Item, class R, bool kWPk = false, int kC = kWCap>
 struct SortLayout {
     static constexpr int NACC = ItemTraits<Item>::var ? (ItemTraits<Item>::sum ? 3 : 2) : 1;
+    static constexpr uint32_t CAP = kC;
     static constexpr size_t PIDC = 0;                  // records per pid slot
     static constexpr size_t PIDV = PIDC + 4 * kWCq;    // pid hash
     static constexpr size_t CBND = PIDV + 4 * kWCq;    // candidate bound
@@ -80,32 +87,62 @@ struct SortLayout {
     static constexpr size_t FULL = PBASE + 4 * kWCq;   // pid shows >= mpc candidate pairs
     // first position per pair (u16); before the sort: occupied pid slots (u32)
     static constexpr size_t PSTART = FULL + 4 * kWCq;
-    static constexpr size_t CK = PSTART + a16(2 * (kWCap + 1) > 4 * kWCq ? 2 * (kWCap + 1) : 4 * kWCq);
-    // candidate keys u64[kWCap] + record indices u32[kWCap]; then record
-    // keys by position (u64); then NACC accumulators per pair (f64)
-    static constexpr size_t CIDX = CK + 8 * kWCap;
-    static constexpr size_t CKSZ = 12 * kWCap > 8 * NACC * kWCap ? 12 * kWCap : 8 * NACC * kWCap;
+    static constexpr size_t CK = PSTART + a16(2 * (kC + 1) > 4 * kWCq ? 2 * (kC + 1) : 4 * kWCq);
+    // candidate keys u64[kC] + record indices u32[kC]; then record keys by
+    // position (u64); then NACC accumulators per pair (f64)
+    static constexpr size_t CIDX = CK + 8 * kC;
+    static constexpr size_t CKSZ = 12 * kC > 8 * NACC * kC ? 12 * kC : 8 * NACC * kC;
     // wide partition keys (kWPk): the low pk bits the sort key has no room
     // for, per candidate (u8)
     static constexpr size_t CPKL = CK + CKSZ;
-    static constexpr size_t END = CPKL + (kWPk ? kWCap : 0);
+    static constexpr size_t END = CPKL + (kWPk ? kC : 0);
     static constexpr size_t TOTAL = (END + 255) & ~(size_t)255;
     static_assert(TOTAL <= 40 * 1024, "sort working set too large");
 };
 
-// Two instantiations of the kernel (kWide):
-//  * narrow: chunks of <= kNarrowCand candidates (E <= 4 elements per lane),
-//    registers for 4 waves per SIMD (<= 128 VGPRs; the bound parameters stay
-//    in scalar registers); a chunk with more candidates is only flagged
-//    (defer[w] = 1) and left to
-//  * wide: E <= 8, 2 waves per SIMD (the 8-element sort network needs ~230
-//    VGPRs), which walks the flagged chunks of the narrow kernel's
-//    workgroups and appends to their item regions.
-// Config 2 (~120 candidates per chunk) never reaches the wide kernel; chunks
-// of many small privacy ids (every record a candidate) do.
-constexpr uint32_t kNarrowCand = 256;
-constexpr int kNarrowWPS = 4;  // waves per SIMD the narrow kernel's registers allow
+// Passes of the kernel over the small-chunk list (kTier):
+//  * 0, narrow: chunks of <= kNarrowCand<R> candidates, a working set sized
+//    for them and registers for kNarrowWPS<R> waves per SIMD; a chunk with
+//    more candidates is only flagged (defer[w] = 1) and left to
+//  * 1, mid (only with a narrow capacity below 256, DPG_NARROW_CAND):
+//    <= 256 candidates (E <= 4 elements per lane), 4 waves per SIMD, over
+//    the flagged chunks of the narrow workgroups; it clears the flags of the
+//    chunks it bounds and leaves the rest to
+//  * 2, wide: E <= 8, 2 waves per SIMD (the 8-element sort network needs
+//    ~230 VGPRs), or the 2-wave kernel of dpg_sortmw.h.
+// The deferred passes walk the flagged chunks of the narrow workgroups and
+// append to their item regions.  With 8-byte records the narrow pass runs
+// at 5 waves per SIMD (96 VGPRs: no next-chunk prefetch, 7 spilled VGPRs)
+// over a working set sized for its 256 candidates (6 KB): same-box A/B at
+// config 2, bounding 6.61-6.64 -> 6.27-6.31 ms per step
+// (profiles/r5/r5w_sort_5wps_ab.txt).  A 128-candidate narrow pass (4.5 KB,
+// 96 VGPRs without spills) bounds the chunks it keeps faster still, but
+// about half of config 2's chunks hold more than 128 candidates, and a mid
+// pass for them costs more than it saves (r5h, r5j).  Chunks of many small
+// privacy ids (every record a candidate) reach the wide pass.
+#ifndef DPG_NARROW_CAND
+#define DPG_NARROW_CAND 256  // 8-byte records; 12-byte ones: 256
+#endif
+#ifndef DPG_NARROW_WPS
+#define DPG_NARROW_WPS 5
+#endif
+template <class R>
+constexpr uint32_t kNarrowCand = sizeof(R) == 8 ? DPG_NARROW_CAND : 256;
+template <class R>
+constexpr int kNarrowWPS = sizeof(R) == 8 ? DPG_NARROW_WPS : 4;  // waves per SIMD by registers
+// the narrow pass loads the next chunk's records during the current one
+// (8-byte records: not at 5 waves per SIMD, where the prefetch registers spill)
+template <class R>
+constexpr bool kSortPF = sizeof(R) == 8 ? DPG_SORT_PF != 0 : true;
+constexpr uint32_t kMidCand = 256;
+constexpr int kMidWPS = 4;
+template <class R>
+constexpr bool kHasMid = kNarrowCand<R> < kMidCand;
 constexpr int kWideWPS = 2;
+template <class R, int kTier>
+constexpr int kTierCand = kTier == 0 ? (int)kNarrowCand<R> : kTier == 1 ? (int)kMidCand : kWCap;
+template <class R, int kTier>
+constexpr int kTierWPS = kTier == 0 ? kNarrowWPS<R> : kTier == 1 ? kMidWPS : kWideWPS;
 #ifndef DPG_SORT_VREG
 #define DPG_SORT_VREG 1  // bound parameters the narrow kernel keeps in VGPRs (0, 1 or 2 groups)
 #endif
@@ -311,11 +348,12 @@ __device__ __forceinline__ void bitonic_sort_keys_f64(uint64_t (&k)[E]) {
 // narrow kernel defers such a chunk (kRoundDefer) to the wide kernel, whose
 // comparator (kLex) orders by (key, payload).
 constexpr int kRoundRestart = 0, kRoundDone = 1, kRoundDefer = 2;
-template <class Item, class R, int E, bool kWPk, bool kLex>
+template <class Item, class R, int E, bool kWPk, bool kLex, int kC>
 __device__ __forceinline__ int sort_chunk(uint32_t nc, char *smem, const BoundParams &bp,
                                            bool last_round, uint32_t hbound, uint32_t hidx,
                                            Item *items, uint32_t &nitems, PhaseTimer &clk) {
-    using L = SortLayout<Item, R, kWPk>;
+    using L = SortLayout<Item, R, kWPk, kC>;
+    static_assert(64 * E <= kC || E == 1, "sort width beyond the working set");
     constexpr bool kVar = ItemTraits<Item>::var;
     constexpr bool kSum = ItemTraits<Item>::sum;
     const uint8_t *cpkl = reinterpret_cast<const uint8_t *>(smem + L::CPKL);
@@ -329,8 +367,8 @@ __device__ __forceinline__ int sort_chunk(uint32_t nc, char *smem, const BoundPa
     uint64_t *rks = ckey;  // after the sort (phase M)
     uint16_t *pstart = reinterpret_cast<uint16_t *>(smem + L::PSTART);
     double *acc = reinterpret_cast<double *>(smem + L::CK);  // phase F
-    double *acc_nsum = acc + (kSum ? kWCap : 0);
-    double *acc_nsq = acc_nsum + kWCap;
+    double *acc_nsum = acc + (kSum ? L::CAP : 0);
+    double *acc_nsq = acc_nsum + L::CAP;
     const uint32_t lane = __lane_id();
     const Fmt f = bp.fmt;
     const bool need_v = bp.need_values != 0;
@@ -346,7 +384,7 @@ __device__ __forceinline__ int sort_chunk(uint32_t nc, char *smem, const BoundPa
 #pragma unroll
     for (int j = 0; j < E; ++j) {
         const uint32_t i = lane * E + j;
-        const uint32_t ic = min(i, (uint32_t)kWCap - 1);
+        const uint32_t ic = min(i, L::CAP - 1);
         const uint64_t x = ckey[ic];
         const uint32_t y = kWPk ? (ic | ((uint32_t)cpkl[ic] << 9)) : cidx[ic];
         k[j] = i < nc ? x : kSkPad;
@@ -382,8 +420,8 @@ __device__ __forceinline__ int sort_chunk(uint32_t nc, char *smem, const BoundPa
         for (int j = 0; j < E; ++j) {
             const uint32_t i = lane * E + j;
             const uint32_t pos = (uint32_t)pk64[j] & 511u;
-            k[j] = i < nc ? ckey[min(pos, (uint32_t)kWCap - 1)] : kSkPad;
-            o[j] = i < nc ? cidx[min(pos, (uint32_t)kWCap - 1)] : 0u;
+            k[j] = i < nc ? ckey[min(pos, L::CAP - 1)] : kSkPad;
+            o[j] = i < nc ? cidx[min(pos, L::CAP - 1)] : 0u;
         }
         const uint64_t pl = (uint64_t)__shfl_up((long long)k[E - 1], 1, 64);
         bool bad = false;
@@ -397,7 +435,7 @@ __device__ __forceinline__ int sort_chunk(uint32_t nc, char *smem, const BoundPa
 #pragma unroll
             for (int j = 0; j < E; ++j) {
                 const uint32_t i = lane * E + j;
-                const uint32_t ic = min(i, (uint32_t)kWCap - 1);
+                const uint32_t ic = min(i, L::CAP - 1);
                 k[j] = i < nc ? ckey[ic] : kSkPad;
                 o[j] = i < nc ? cidx[ic] : 0u;
             }
@@ -485,9 +523,9 @@ __device__ __forceinline__ int sort_chunk(uint32_t nc, char *smem, const BoundPa
     double v[E];
 #pragma unroll
     for (int j = 0; j < E; ++j) {
-        st[j] = pstart[min(a[j], (uint32_t)kWCap - 1)];
-        len[j] = pstart[min(a[j] + 1, (uint32_t)kWCap)];
-        idx[j] = kWPk ? cidx[o[j] & (kWCap - 1)] : o[j];
+        st[j] = pstart[min(a[j], L::CAP - 1)];
+        len[j] = pstart[min(a[j] + 1, L::CAP)];
+        idx[j] = kWPk ? cidx[min(o[j] & 511u, L::CAP - 1)] : o[j];
         pkf[j] = kWPk ? ((((uint32_t)k[j] & kPkMask) << pksh) | (o[j] >> 9)) : ((uint32_t)k[j] & kPkMask);
     }
     uint32_t overm = 0, maxlen = 0;
@@ -523,8 +561,8 @@ __device__ __forceinline__ int sort_chunk(uint32_t nc, char *smem, const BoundPa
             const uint32_t lm = max(len[j], 1u) - 1u;
             uint32_t below = 0;
             for (uint32_t t = 0; t < maxlen; t += 2) {
-                const uint64_t y0 = rks[min(st[j] + min(t, lm), (uint32_t)kWCap - 1)];
-                const uint64_t y1 = rks[min(st[j] + min(t + 1, lm), (uint32_t)kWCap - 1)];
+                const uint64_t y0 = rks[min(st[j] + min(t, lm), L::CAP - 1)];
+                const uint64_t y1 = rks[min(st[j] + min(t + 1, lm), L::CAP - 1)];
                 below += (t < len[j] && y0 < mine) ? 1u : 0u;
                 below += (t + 1 < len[j] && y1 < mine) ? 1u : 0u;
             }
@@ -598,14 +636,14 @@ __device__ __forceinline__ int sort_chunk(uint32_t nc, char *smem, const BoundPa
 // One round: (first round only) records per pid slot, pid hashes and
 // candidate bounds; pair priorities; candidates compacted into LDS; sort and
 // bound.  Returns kRoundDone, kRoundRestart (see sort_chunk) or, in the
-// narrow kernel, kRoundDefer (more than kNarrowCand candidates, or a key
+// narrow and mid passes, kRoundDefer (more than kC candidates, or a key
 // collision of wide partition keys).
-template <class Item, class R, bool kFirst, bool kWide, bool kWPk>
+template <class Item, class R, bool kFirst, bool kWide, bool kWPk, int kC>
 __device__ __forceinline__ int sort_round(const R (&r)[kWRPT], uint32_t n, uint32_t d1,
                                            uint32_t hbase, char *smem, const BoundParams &bp,
                                            Item *items, uint32_t &nitems, PhaseTimer &clk,
                                            uint32_t hbound, uint32_t hidx) {
-    using L = SortLayout<Item, R, kWPk>;
+    using L = SortLayout<Item, R, kWPk, kC>;
     uint32_t *pidv = reinterpret_cast<uint32_t *>(smem + L::PIDV);
     uint32_t *pidc = reinterpret_cast<uint32_t *>(smem + L::PIDC);
     uint32_t *cbnd = reinterpret_cast<uint32_t *>(smem + L::CBND);
@@ -680,8 +718,10 @@ __device__ __forceinline__ int sort_round(const R (&r)[kWRPT], uint32_t n, uint3
             sk[k] |= (uint64_t)pp << kSkPkBits;
             const bool c = ((validm >> k) & 1u) && pp <= cb[k];
             const uint64_t bc = __ballot(c);
-            if (c) {
-                const uint32_t e = nc + lanes_below(bc);
+            // the working set holds kC candidates: past them the chunk is
+            // deferred below (narrow and mid passes), so the rest need no slot
+            const uint32_t e = nc + lanes_below(bc);
+            if (c && e < L::CAP) {
                 ckey[e] = sk[k];
                 cidx[e] = ix[k];
                 if constexpr (kWPk) cpkl[e] = (uint8_t)(pk & ((1u << pksh) - 1u));
@@ -692,20 +732,23 @@ __device__ __forceinline__ int sort_round(const R (&r)[kWRPT], uint32_t n, uint3
     wave_sync();
     mark(bp, 0, clk);
     if constexpr (!kWide) {
-        if (nc > kNarrowCand) return kRoundDefer;
+        if (nc > (uint32_t)kC) return kRoundDefer;
     }
     constexpr bool last = !kFirst;
     constexpr bool kLex = kWide && kWPk;
     int st;
-    if (nc <= 64)
-        st = sort_chunk<Item, R, 1, kWPk, kLex>(nc, smem, bp, last, hbound, hidx, items, nitems, clk);
-    else if (nc <= 128)
-        st = sort_chunk<Item, R, 2, kWPk, kLex>(nc, smem, bp, last, hbound, hidx, items, nitems, clk);
-    else if (!kWide || nc <= 256)
-        st = sort_chunk<Item, R, 4, kWPk, kLex>(nc, smem, bp, last, hbound, hidx, items, nitems, clk);
-    else
-        st = sort_chunk<Item, R, kWide ? 8 : 4, kWPk, kLex>(nc, smem, bp, last, hbound, hidx, items,
-                                                            nitems, clk);
+    if (nc <= 64) {
+        st = sort_chunk<Item, R, 1, kWPk, kLex, L::CAP>(nc, smem, bp, last, hbound, hidx, items, nitems, clk);
+    } else if (nc <= 128 || (!kWide && kC <= 128)) {
+        st = sort_chunk<Item, R, 2, kWPk, kLex, L::CAP>(nc, smem, bp, last, hbound, hidx, items, nitems, clk);
+    } else if constexpr (kWide || kC > 128) {
+        if (!kWide || nc <= 256)
+            st = sort_chunk<Item, R, 4, kWPk, kLex, L::CAP>(nc, smem, bp, last, hbound, hidx, items, nitems,
+                                                    clk);
+        else
+            st = sort_chunk<Item, R, kWide ? 8 : 4, kWPk, kLex, L::CAP>(nc, smem, bp, last, hbound, hidx,
+                                                                items, nitems, clk);
+    }
     wave_sync();
     return st;
 }
@@ -716,22 +759,22 @@ __device__ __forceinline__ int sort_round(const R (&r)[kWRPT], uint32_t n, uint3
 // registers across the sort would cost the occupancy the kernel lives on.
 // Returns true when the chunk was deferred to the wide kernel (nothing
 // emitted).
-template <class Item, class R, bool kWide, bool kWPk>
+template <class Item, class R, bool kWide, bool kWPk, int kC>
 __device__ __forceinline__ bool sort_bound_chunk(const R (&r0)[kWRPT], const R *base, uint32_t n,
                                                  uint32_t d1, uint32_t hbase, char *smem,
                                                  const BoundParams &bp, Item *items,
                                                  uint32_t &nitems, PhaseTimer &clk,
                                                  uint32_t hbound, uint32_t hidx) {
-    using L = SortLayout<Item, R, kWPk>;
+    using L = SortLayout<Item, R, kWPk, kC>;
     uint32_t *pidc = reinterpret_cast<uint32_t *>(smem + L::PIDC);
     const uint32_t lane = __lane_id();
-    int st = sort_round<Item, R, true, kWide, kWPk>(r0, n, d1, hbase, smem, bp, items, nitems, clk,
+    int st = sort_round<Item, R, true, kWide, kWPk, kC>(r0, n, d1, hbase, smem, bp, items, nitems, clk,
                                               hbound, hidx);
     if (st == kRoundRestart) {
         R r[kWRPT];
 #pragma unroll
         for (int k = 0; k < kWRPT; ++k) r[k] = base[min(lane + 64u * k, n - 1)];
-        st = sort_round<Item, R, false, kWide, kWPk>(r, n, d1, hbase, smem, bp, items, nitems, clk,
+        st = sort_round<Item, R, false, kWide, kWPk, kC>(r, n, d1, hbase, smem, bp, items, nitems, clk,
                                                hbound, hidx);
     }
 #pragma unroll
@@ -744,16 +787,19 @@ __device__ __forceinline__ bool sort_bound_chunk(const R (&r0)[kWRPT], const R *
 // Persistent single-wave workgroups walk the small-chunk list statically
 // (w, w + G1, ...), as k_bound_waves; narrow workgroup g appends its items
 // to items[wg_off[g], ...) and leaves the count in wg_cnt[g], and flags the
-// chunks it defers in defer[w].  The wide kernel's workgroup g2 then takes
+// chunks it defers in defer[w].  A deferred pass's workgroup g2 then takes
 // the narrow workgroups g = g2, g2 + gridDim.x, ... and bounds their flagged
-// chunks, appending behind wg_cnt[g].  The narrow kernel loads the next
-// chunk's records while the current one is bounded.
-template <class Item, class R, bool kWide, bool kWPk>
-__global__ __launch_bounds__(64, kWide ? kWideWPS : kNarrowWPS) void k_bound_sorted(
+// chunks, appending behind wg_cnt[g] (the mid pass clears the flag of a
+// chunk it bounds).  The narrow pass may load the next chunk's records while
+// the current one is bounded (kSortPF).
+template <class Item, class R, int kTier, bool kWPk>
+__global__ __launch_bounds__(64, (kTierWPS<R, kTier>)) void k_bound_sorted(
     const R *recs, const R *refined, const R *heavy, const uint4 *chunks, const uint32_t *n_chunks,
     BoundParams bp, Item *items, const int64_t *wg_off, uint32_t *wg_cnt, uint8_t *defer,
     uint32_t G1) {
-    using L = SortLayout<Item, R, kWPk>;
+    constexpr bool kWide = kTier == 2;
+    constexpr int kC = kTierCand<R, kTier>;
+    using L = SortLayout<Item, R, kWPk, kC>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     PhaseTimer clk;
     timer_start(bp, clk);
@@ -799,7 +845,8 @@ __global__ __launch_bounds__(64, kWide ? kWideWPS : kNarrowWPS) void k_bound_sor
                           __builtin_amdgcn_readfirstlane(chunks[w].z),
                           __builtin_amdgcn_readfirstlane(chunks[w].w));
     };
-    if constexpr (!kWide) {
+    if constexpr (kTier == 0) {
+        constexpr bool kPF = kSortPF<R>;
         uint32_t nitems = 0;
         Item *my_items = items + wg_off[blockIdx.x];
         R r[kWRPT], rn[kWRPT];
@@ -813,20 +860,28 @@ __global__ __launch_bounds__(64, kWide ? kWideWPS : kNarrowWPS) void k_bound_sor
         }
         for (uint32_t w = blockIdx.x; w < nch; w += G1) {
             uint4 du = make_uint4(0, 0, 0, 0);
-            if (w + G1 < nch) {
+            if (kPF && w + G1 < nch) {
                 du = desc(w + G1);
                 const uint32_t nn = du.y & kChunkCount;
                 const R *nb = wave_chunk_base(du, recs, refined, heavy);
 #pragma unroll
                 for (int k = 0; k < kWRPT; ++k) rn[k] = nb[min(lane + 64u * k, nn - 1)];
             }
-            const bool df = sort_bound_chunk<Item, R, false, kWPk>(
+            const bool df = sort_bound_chunk<Item, R, false, kWPk, kC>(
                 r, wave_chunk_base(d, recs, refined, heavy), d.y & kChunkCount, d.z & 0xFFFFu, d.w,
                 smem, bp, my_items, nitems, clk, heavy_bound(d), d.x / (uint32_t)kWCap);
             if (lane == 0) defer[w] = df ? 1 : 0;
+            if constexpr (kPF) {
 #pragma unroll
-            for (int k = 0; k < kWRPT; ++k) r[k] = rn[k];
-            d = du;
+                for (int k = 0; k < kWRPT; ++k) r[k] = rn[k];
+                d = du;
+            } else if (w + G1 < nch) {
+                d = desc(w + G1);
+                const uint32_t nn = d.y & kChunkCount;
+                const R *nb = wave_chunk_base(d, recs, refined, heavy);
+#pragma unroll
+                for (int k = 0; k < kWRPT; ++k) r[k] = nb[min(lane + 64u * k, nn - 1)];
+            }
         }
         if (lane == 0) wg_cnt[blockIdx.x] = nitems;
     } else {
@@ -847,9 +902,10 @@ __global__ __launch_bounds__(64, kWide ? kWideWPS : kNarrowWPS) void k_bound_sor
                     R r[kWRPT];
 #pragma unroll
                     for (int k = 0; k < kWRPT; ++k) r[k] = b[min(lane + 64u * k, n - 1)];
-                    sort_bound_chunk<Item, R, true, kWPk>(r, b, n, d.z & 0xFFFFu, d.w, smem, bp, my_items,
-                                                    nitems, clk, heavy_bound(d),
-                                                    d.x / (uint32_t)kWCap);
+                    const bool df = sort_bound_chunk<Item, R, kWide, kWPk, kC>(
+                        r, b, n, d.z & 0xFFFFu, d.w, smem, bp, my_items, nitems, clk,
+                        heavy_bound(d), d.x / (uint32_t)kWCap);
+                    if (kTier == 1 && lane == 0) defer[w] = df ? 1 : 0;
                 }
             }
             if (any && lane == 0) wg_cnt[g] = nitems;
