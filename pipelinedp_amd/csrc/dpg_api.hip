@@ -22,9 +22,46 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <string>
 #include <thread>
+#include <tuple>
 #include <vector>
+
+// Occupancy and the dynamic-LDS attribute are fixed per (device, kernel,
+// block size, LDS): looked up and set once per process.  A release makes
+// ~10 of these calls, several right after a host synchronisation, where
+// host time is GPU idle time.
+static hipError_t occ_query(int *blocks, const void *kern, int threads, size_t lds) {
+    static std::mutex mu;
+    static std::map<std::tuple<int, const void *, int, size_t>, int> cache;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> g(mu);
+    const auto key = std::make_tuple(dev, kern, threads, lds);
+    const auto it = cache.find(key);
+    if (it != cache.end()) {
+        *blocks = it->second;
+        return hipSuccess;
+    }
+    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, kern, threads, lds);
+    if (e == hipSuccess) cache[key] = *blocks;
+    return e;
+}
+static hipError_t set_func_attr(const void *kern, hipFuncAttribute attr, int value) {
+    if (attr != hipFuncAttributeMaxDynamicSharedMemorySize) return hipFuncSetAttribute(kern, attr, value);
+    static std::mutex mu;
+    static std::map<std::pair<int, const void *>, int> done;  // largest value set
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> g(mu);
+    const auto key = std::make_pair(dev, kern);
+    const auto it = done.find(key);
+    if (it != done.end() && it->second >= value) return hipSuccess;
+    const hipError_t e = hipFuncSetAttribute(kern, attr, value);
+    if (e == hipSuccess) done[key] = value;
+    return e;
+}
 
 #include "dpg_bound.h"
 #include "dpg_chunk.h"
@@ -389,7 +426,7 @@ int run_level_grouped(dpg_ctx *ctx, hipStream_t s, const Src &src, uint32_t S,
                                                              xq);
     LAUNCH_CHECK();
     if (F > 2048)
-        (void)hipFuncSetAttribute((const void *)k_hist<Src>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)set_func_attr((const void *)k_hist<Src>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)(4 * F * sizeof(uint32_t)));
     k_hist<Src><<<max_groups, kPartThreads, 4 * F * sizeof(uint32_t), s>>>(src, groups, ngrp, F, hist);
     LAUNCH_CHECK();
@@ -408,7 +445,7 @@ int run_level_grouped(dpg_ctx *ctx, hipStream_t s, const Src &src, uint32_t S,
     constexpr size_t lds = scatter_lds<Src, Rec, IPT, FMAX>();
     static_assert(lds <= 160 * 1024, "scatter LDS");
     auto kern = bits > agg_bits() ? k_scatter<Src, Rec, IPT, FMAX, false> : k_scatter<Src, Rec, IPT, FMAX, true>;
-    (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)set_func_attr((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
     stage(ctx, s, (t + ":scatter").c_str());
     const uint32_t gs = std::min<uint32_t>(max_subs, (uint32_t)ctx->n_cu);  // one per CU
@@ -479,7 +516,7 @@ int run_level(dpg_ctx *ctx, hipStream_t s, const Src &src, uint32_t S, const int
     }
     LAUNCH_CHECK();
     if (F > 2048)
-        (void)hipFuncSetAttribute((const void *)k_hist<Src>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)set_func_attr((const void *)k_hist<Src>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)(4 * F * sizeof(uint32_t)));
     k_hist<Src><<<max_tiles, kPartThreads, 4 * F * sizeof(uint32_t), s>>>(src, tiles, ntiles_dev,
                                                                           F, hist);
@@ -496,7 +533,7 @@ int run_level(dpg_ctx *ctx, hipStream_t s, const Src &src, uint32_t S, const int
     static_assert(lds <= 160 * 1024, "scatter LDS");
     // few digits: wave-aggregated ranking; otherwise one LDS atomic per record
     auto kern = bits > agg_bits() ? k_scatter<Src, Rec, IPT, FMAX, false> : k_scatter<Src, Rec, IPT, FMAX, true>;
-    (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)set_func_attr((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
     stage(ctx, s, (t + ":scatter").c_str());
 #ifndef DPG_SCAT_WGS
@@ -728,7 +765,7 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     // 42 ms, 4 per CU 29.7 ms)
     auto waves_per_cu = [&](const void *kern, size_t lds, int cap = 16) {
         int wpc = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&wpc, kern, 64, lds) != hipSuccess ||
+        if (occ_query(&wpc, kern, 64, lds) != hipSuccess ||
             wpc <= 0)
             wpc = 1;
         int pc = std::min(wpc, (int)std::min<size_t>((size_t)cap, (160 * 1024) / lds));
@@ -743,7 +780,7 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     const bool use_mw = use_sort && pl.plb <= 7 && std::getenv("DPG_MW_OFF") == nullptr;
     auto blocks_per_cu = [&](const void *kern, int threads, size_t lds) {
         int b = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, threads, lds) != hipSuccess ||
+        if (occ_query(&b, kern, threads, lds) != hipSuccess ||
             b <= 0)
             b = 1;
         return b;
@@ -812,9 +849,9 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     stage(ctx, s, "bound");
     if constexpr (!ItemTraits<Item>::preagg) if (use_sort) {
         WS(defer, uint8_t, "bound.defer", std::max<size_t>(chunk_cap, 1));
-        (void)hipFuncSetAttribute(narrow, hipFuncAttributeMaxDynamicSharedMemorySize, (int)wave_lds);
-        if (mid) (void)hipFuncSetAttribute(mid, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mid_lds);
-        (void)hipFuncSetAttribute(wide, hipFuncAttributeMaxDynamicSharedMemorySize, (int)wide_lds);
+        (void)set_func_attr(narrow, hipFuncAttributeMaxDynamicSharedMemorySize, (int)wave_lds);
+        if (mid) (void)set_func_attr(mid, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mid_lds);
+        (void)set_func_attr(wide, hipFuncAttributeMaxDynamicSharedMemorySize, (int)wide_lds);
         auto launch = [&](auto wpk_tag) {
             constexpr bool W = decltype(wpk_tag)::value;
             k_bound_sorted<Item, R, 0, W><<<Gw, 64, wave_lds, s>>>(
@@ -839,7 +876,7 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
                 if (timing) bpx.phase_cyc = bpl.phase_cyc + 48;
                 using LW = SortLayoutMW<Item, R, W, 2>;
                 const void *k2 = (const void *)k_bound_sorted_w2<Item, R, W>;
-                (void)hipFuncSetAttribute(k2, hipFuncAttributeMaxDynamicSharedMemorySize,
+                (void)set_func_attr(k2, hipFuncAttributeMaxDynamicSharedMemorySize,
                                           (int)LW::TOTAL);
                 const uint32_t Gx = std::min<uint32_t>(
                     Gw, (uint32_t)(ctx->n_cu * blocks_per_cu(k2, LW::T, LW::TOTAL)));
@@ -862,7 +899,7 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
         LAUNCH_CHECK();
     }
     if (!use_sort) {
-        (void)hipFuncSetAttribute((const void *)wave_kern,
+        (void)set_func_attr((const void *)wave_kern,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)wave_lds);
         wave_kern<<<Gw, 64, wave_lds, s>>>(recs, refined, hrec, chunk_list, &ctl->n_chunks, bpl,
                                            items, wg_off, wg_cnt);
@@ -879,7 +916,7 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
             auto launch_m = [&](auto wpk_tag) {
                 constexpr bool W = decltype(wpk_tag)::value;
                 using LM = SortLayoutMW<Item, R, W, 4>;
-                (void)hipFuncSetAttribute((const void *)k_bound_sorted_m4<Item, R, W>,
+                (void)set_func_attr((const void *)k_bound_sorted_m4<Item, R, W>,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)LM::TOTAL);
                 BoundParams bpm = bpl;
                 if (timing) bpm.phase_cyc = bpl.phase_cyc + 16;
@@ -901,7 +938,7 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
         BoundParams bpm = bpl;
         if (timing) bpm.phase_cyc = bpl.phase_cyc + 16;
         if (prog) bpm.progress = prog + Gw;
-        (void)hipFuncSetAttribute((const void *)k_bound_chunks<KeyT, Item, R>,
+        (void)set_func_attr((const void *)k_bound_chunks<KeyT, Item, R>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)CL::TOTAL);
         k_bound_chunks<KeyT, Item, R><<<Gm, kBT, CL::TOTAL, s>>>(
             recs, refined, mchunk_list, &ctl->n_mchunks, bpm, items, wg_off + Gw, wg_cnt + Gw);
@@ -1196,7 +1233,7 @@ int run_level1_pieces(dpg_ctx *ctx, hipStream_t s, const SrcSoAKey<R, true> &src
     static_assert(lds <= 160 * 1024, "scatter LDS");
     auto kern = k_scatter<Src, R, IPT, 2048, false>;
     if (bits <= (uint32_t)agg_bits()) return fail(ctx, DPG_ERR_HIP, "internal: piece level fan-out");
-    (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)set_func_attr((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
     const uint32_t gs = std::min<uint32_t>(nt, (uint32_t)ctx->n_cu);  // one per CU
     if (int r = scat_phase_begin(ctx, s)) return r;
@@ -1242,7 +1279,7 @@ int run_team_level2(dpg_ctx *ctx, hipStream_t s, const SrcAoS<R> &src, uint32_t 
         LAUNCH_CHECK();
     }
     const void *k = pt ? (const void *)k_part2_team<R, true> : (const void *)k_part2_team<R, false>;
-    (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)team_lds<R>());
+    (void)set_func_attr(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)team_lds<R>());
     stage(ctx, s, "partition2:team");
     if (pt)
         k_part2_team<R, true><<<(unsigned)ctx->n_cu, kScatThreads, team_lds<R>(), s>>>(
@@ -1313,9 +1350,9 @@ int pipeline(dpg_ctx *ctx, hipStream_t s, const int64_t *pid, const int64_t *pk,
     if constexpr (sizeof(R) == 8) if (team) {
         int occ = 0;
         const void *tk = (const void *)k_part2_team<R>;
-        (void)hipFuncSetAttribute(tk, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)set_func_attr(tk, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)team_lds<R>());
-        team = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, tk, kScatThreads,
+        team = occ_query(&occ, tk, kScatThreads,
                                                             team_lds<R>()) == hipSuccess &&
                occ >= 1;
     }
@@ -2100,10 +2137,10 @@ int dpg_utility_analysis(dpg_ctx *ctx, const dpg_pair_entry *pairs,
         // resident waves of the full table), then the others
         const size_t lds_x = (size_t)kPgfB * kPgfNB * a.n_cls * 8;
         auto launch = [&](auto kern, size_t l) {
-            (void)hipFuncSetAttribute((const void *)kern,
+            (void)set_func_attr((const void *)kern,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)l);
             int occ = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void *)kern, 64, l) !=
+            if (occ_query(&occ, (const void *)kern, 64, l) !=
                     hipSuccess || occ < 1)
                 occ = 4;
             const unsigned g = (unsigned)std::min<int64_t>(P, (int64_t)ctx->n_cu * occ);
@@ -2245,7 +2282,7 @@ int dpg_dataset_histograms(dpg_ctx *ctx, const dpg_pair_entry *pairs, int64_t n_
     k_hist_lowers<<<(kHsBins + kHistThreads) / kHistThreads, kHistThreads, 0, s>>>(a);
     LAUNCH_CHECK();
     const size_t lds = (size_t)kHsBins * (4 + 8);
-    (void)hipFuncSetAttribute((const void *)k_hist_sums, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)set_func_attr((const void *)k_hist_sums, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
     k_hist_sums<<<(unsigned)std::min<int64_t>((n_pairs + 1023) / 1024, (int64_t)ctx->n_cu), 1024,
                   lds, s>>>(pa, n_pairs, a);
