@@ -144,7 +144,7 @@ constexpr int kTierCand = kTier == 0 ? (int)kNarrowCand<R> : kTier == 1 ? (int)k
 template <class R, int kTier>
 constexpr int kTierWPS = kTier == 0 ? kNarrowWPS<R> : kTier == 1 ? kMidWPS : kWideWPS;
 #ifndef DPG_SORT_VREG
-#define DPG_SORT_VREG 1  // bound parameters the narrow kernel keeps in VGPRs (0, 1 or 2 groups)
+#define DPG_SORT_VREG 0  // bound parameters the narrow kernel keeps in VGPRs (0, 1 or 2 groups; 5 waves per SIMD: 0, r5z)
 #endif
 
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
