@@ -558,11 +558,17 @@ struct Ipt {
 #ifndef DPG_IPT_L1
 #define DPG_IPT_L1 11  // same-box A/B config 2: 12 -> 11 level-1 scatter 7.88 -> 7.25 ms (spills)
 #endif
-    static constexpr int L1 = sizeof(R) == 8 ? DPG_IPT_L1 : sizeof(R) == 16 ? 7 : 8;
+#ifndef DPG_IPT_L1_R16
+#define DPG_IPT_L1_R16 7  // the utility pre-aggregate's 16-byte records
+#endif
+    static constexpr int L1 = sizeof(R) == 8 ? DPG_IPT_L1 : sizeof(R) == 16 ? DPG_IPT_L1_R16 : 8;
 #ifndef DPG_IPT_LN
 #define DPG_IPT_LN 12  // same-box A/B config 2: 16 -> 12 level-2 scatter 5.97 -> 4.37 ms (spills)
 #endif
-    static constexpr int LN = sizeof(R) == 8 ? DPG_IPT_LN : sizeof(R) == 16 ? 8 : 10;
+#ifndef DPG_IPT_LN_R16
+#define DPG_IPT_LN_R16 8
+#endif
+    static constexpr int LN = sizeof(R) == 8 ? DPG_IPT_LN : sizeof(R) == 16 ? DPG_IPT_LN_R16 : 10;
     // the refine level has few digits (wave-aggregated ranking, which holds
     // more registers per record: at LN records per thread it spilled)
     static constexpr int LR = sizeof(R) == 8 ? 8 : 6;
@@ -1059,7 +1065,10 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
                                               ((uint64_t)1 << pl.kbits) * pairs_per_id);
     }
     const int64_t P = pl.P;
-    constexpr int kItemIpt = sizeof(Item) == 16 ? 8 : 4;
+#ifndef DPG_ITEM_IPT_WIDE
+#define DPG_ITEM_IPT_WIDE 4  // 24-byte items per thread per sub-tile (LDS caps it at 5)
+#endif
+    constexpr int kItemIpt = sizeof(Item) == 16 ? 8 : sizeof(Item) == 24 ? DPG_ITEM_IPT_WIDE : 4;
     // the items are partitioned by partition-key range: one level up to 1024
     // ranges, else two (pk >> (rbits + b2), then (pk >> rbits) mod 2^b2) --
     // the final segment index is the range id either way
