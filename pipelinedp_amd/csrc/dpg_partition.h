@@ -25,7 +25,7 @@ namespace dpg {
 #define DPG_HIST_U 8
 #endif
 #ifndef DPG_SCAT_WB
-#define DPG_SCAT_WB 4  // same-box A/B: 8 -> 4 level-1 scatter 7.51 -> 7.45 ms (fewer live registers)
+#define DPG_SCAT_WB 2  // same-box A/B: 8 -> 4 level-1 scatter 7.51 -> 7.45 ms, 4 -> 2 pieces 7.24 -> 7.07 ms (r5zd; fewer live registers)
 #endif
 constexpr int kPartThreads = 1024;  // 16 waves
 // scatter workgroups (512 threads with twice the records per thread measured
