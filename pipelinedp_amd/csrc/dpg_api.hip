@@ -88,7 +88,7 @@ constexpr uint32_t kChunkGroup = 32;     // fine buckets per packing thread
 // 8): the caller redoes level 2 with the histogram path.
 constexpr int kRedoLevel2 = -100;
 #ifndef DPG_IPT_PC
-#define DPG_IPT_PC 10  // records per thread of the histogram-free level 1
+#define DPG_IPT_PC 9  // records per thread of the histogram-free level 1 (10 spills: the spill reload waits for the run reservation right after issuing it)
 #endif
 
 struct Buf {
@@ -140,10 +140,13 @@ struct dpg_ctx {
     // runs (the team level-2 decision, see pipeline())
     uint32_t *pin_tot = nullptr;
     hipEvent_t tot_ev = nullptr;
-    // a team level-2 barrier timed out once on this context (workgroups not
-    // co-resident: other work shares the GPU): later calls take the
-    // histogram level 2 directly instead of paying the timeout again
-    bool team_timed_out = false;
+    // a team level-2 barrier timed out on this context (workgroups not
+    // co-resident: other work shares the GPU): the next team_backoff calls
+    // take the histogram level 2 directly instead of paying the timeout
+    // again (stage "team_backoff" marks them); then the team path is tried
+    // again.  Each further timeout doubles the back-off (64 .. 4096 calls).
+    uint32_t team_backoff = 0;
+    uint32_t team_backoff_next = 64;
 };
 
 namespace {
@@ -1169,9 +1172,11 @@ __global__ void k_region_base(int64_t *rbase, uint32_t F, uint32_t C) {
 
 // Bucket totals of the pieces and the buckets' starts in the compact level-2
 // output (one workgroup; F <= 2048).
-__global__ __launch_bounds__(1024) void k_piece_totals(const uint32_t *cum, uint32_t F,
-                                                       uint32_t *tot, uint32_t *ptot,
-                                                       int64_t *ostart) {
+// desc[d]: the bucket's pieces in one record for the team level 2's scalar
+// loads (dpg_team.h PieceDesc).
+__global__ __launch_bounds__(1024) void k_piece_totals(const uint32_t *cum, const int64_t *rbase,
+                                                       uint32_t F, uint32_t *tot, uint32_t *ptot,
+                                                       int64_t *ostart, PieceDesc *desc) {
     __shared__ uint32_t sh[16];
     const uint32_t d0 = 2 * threadIdx.x;
     uint32_t c[2], x = 0;
@@ -1179,13 +1184,22 @@ __global__ __launch_bounds__(1024) void k_piece_totals(const uint32_t *cum, uint
     for (int u = 0; u < 2; ++u) {
         c[u] = 0;
         uint32_t cp = 0;  // padded: each piece rounded up to even (team pair loads)
-        if (d0 + u < F)
+        if (d0 + u < F) {
+            const uint32_t d = d0 + u;
+            const int64_t b0 = rbase[d];
+            PieceDesc &pd = desc[d];
             for (int r = 0; r < 8; ++r) {
-                const uint32_t y = cum[(size_t)r * F + d0 + u];
+                const uint32_t y = cum[(size_t)r * F + d];
+                pd.ppre[r] = cp;
+                pd.dl[r] = (uint32_t)(rbase[(size_t)r * F + d] - b0) - cp;
+                pd.cend[r] = cp + y;
                 c[u] += y;
                 cp += (y + 1u) & ~1u;
             }
-        if (d0 + u < F) ptot[d0 + u] = cp;
+            pd.n = cp;
+            pd.base0 = b0;
+            ptot[d] = cp;
+        }
         x += c[u];
     }
     uint32_t total;
@@ -1195,6 +1209,7 @@ __global__ __launch_bounds__(1024) void k_piece_totals(const uint32_t *cum, uint
         if (d0 + u < F) {
             tot[d0 + u] = c[u];
             ostart[d0 + u] = e;
+            desc[d0 + u].ostart = e;
         }
         e += c[u];
     }
@@ -1229,6 +1244,7 @@ int run_level1_pieces(dpg_ctx *ctx, hipStream_t s, const SrcSoAKey<R, true> &src
     WS(tot, uint32_t, "pieces.tot", F);
     WS(ptot, uint32_t, "pieces.ptot", F);
     WS(ostart, int64_t, "pieces.ostart", F);
+    WS(pdesc, PieceDesc, "pieces.desc", F);
     HIP_TRY(hipMemsetAsync(cum, 0, (size_t)8 * F * 4, s));
     HIP_TRY(hipMemsetAsync(&ctl->ntiles[0], 0, 4, s));
     stage(ctx, s, "partition1:pieces");
@@ -1251,7 +1267,7 @@ int run_level1_pieces(dpg_ctx *ctx, hipStream_t s, const SrcSoAKey<R, true> &src
                                        (uint32_t)((uint64_t)8 * F * C), &ctl->err);
     LAUNCH_CHECK();
     if (int r = scat_phase_end(ctx, s, "partition1:pieces", gs)) return r;
-    k_piece_totals<<<1, 1024, 0, s>>>(cum, F, tot, ptot, ostart);
+    k_piece_totals<<<1, 1024, 0, s>>>(cum, rbase, F, tot, ptot, ostart, pdesc);
     LAUNCH_CHECK();
     // totals and the error word reach the host for the overflow / team checks
     if (!ctx->tot_ev && hipEventCreateWithFlags(&ctx->tot_ev, hipEventDisableTiming) != hipSuccess)
@@ -1259,7 +1275,7 @@ int run_level1_pieces(dpg_ctx *ctx, hipStream_t s, const SrcSoAKey<R, true> &src
     HIP_TRY(hipMemcpyAsync(host_tot, tot, (size_t)F * 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipMemcpyAsync(host_tot + 4095, &ctl->err, 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipEventRecord(ctx->tot_ev, s));
-    *pt = PieceTab{rbase, cum, tot, ptot, ostart, F};
+    *pt = PieceTab{rbase, cum, tot, ptot, ostart, F, pdesc};
     return DPG_OK;
 }
 
@@ -1353,8 +1369,13 @@ int pipeline(dpg_ctx *ctx, hipStream_t s, const int64_t *pid, const int64_t *pk,
     // while the level-1 scatter runs -- every level-1 bucket within a team's
     // registers.  DPG_TEAM_L2=0: the grouped histogram path.
     const uint32_t team_T = (uint32_t)ctx->n_cu / 8;
+    const bool backoff = ctx->team_backoff > 0;
+    if (backoff) {
+        --ctx->team_backoff;
+        stage(ctx, s, "team_backoff");  // visible in the stage times (bench lines)
+    }
     bool team = sizeof(R) == 8 && pl.b2 >= 6 && pl.b2 <= kMaxB1 && ctx->n_cu % 8 == 0 && team_T > 0 && l1_grp &&
-                env_int("DPG_TEAM_L2", 1) != 0 && !ctx->team_timed_out;
+                env_int("DPG_TEAM_L2", 1) != 0 && !backoff;
     if constexpr (sizeof(R) != 8) team = false;
     if constexpr (sizeof(R) == 8) if (team) {
         int occ = 0;
@@ -1519,8 +1540,12 @@ int pipeline(dpg_ctx *ctx, hipStream_t s, const int64_t *pid, const int64_t *pk,
         // a team barrier timed out (workgroups not co-resident): level 2 again
         // with the histogram path, the chunk counters reset
         std::fprintf(stderr, "[dpg] team level 2 timed out; redone with the histogram path "
-                             "(and on this context from now on)\n");
-        ctx->team_timed_out = true;
+                             "(and on this context for the next %u calls)\n",
+                     ctx->team_backoff_next);
+        ctx->team_backoff = ctx->team_backoff_next;
+        if (const char *e = std::getenv("DPG_DEBUG_TEAM_BACKOFF"))  // test hook
+            ctx->team_backoff = (uint32_t)std::max(0, std::atoi(e));
+        ctx->team_backoff_next = std::min<uint32_t>(2 * ctx->team_backoff_next, 4096);
         // a stage of its own, so that stage times (bench lines) show the redo
         stage(ctx, s, "partition2:team_redo");
         HIP_TRY(hipMemsetAsync(&ctl->err, 0, 4, s));
@@ -2065,14 +2090,22 @@ int dpg_utility_analysis(dpg_ctx *ctx, const dpg_pair_entry *pairs,
     for (int k = 0; k < a.n_cls; ++k) {
         const UaConfig &r = hc[cls_rep[k]];
         const int64_t sh = r.pre_threshold > 0 ? r.pre_threshold - 1 : 0;
+        // the bound is clamped in double before the conversion (an extreme
+        // epsilon / delta gives a huge or non-finite threshold or scale, whose
+        // conversion to int64 would be undefined): past the table cap, any
+        // value gives the same npi
+        auto cap_count = [](double x) -> int64_t {
+            return std::isfinite(x) ? (int64_t)std::min(std::max(x, 0.0), (double)INT32_MAX)
+                                    : (int64_t)INT32_MAX;
+        };
         int64_t i1;
         if (r.strategy == DPG_SELECT_TRUNCATED_GEOMETRIC)
             i1 = r.table_len - 1 + sh;
         else if (r.strategy == DPG_SELECT_LAPLACE_THRESHOLD)
-            i1 = (int64_t)std::ceil(r.threshold + 37.5 * r.scale) + sh;
+            i1 = cap_count(std::ceil(r.threshold + 37.5 * r.scale)) + sh;
         else
-            i1 = (int64_t)std::ceil(r.threshold + 8.5 * r.scale) + sh;
-        top = std::max(top, i1 + 1);
+            i1 = cap_count(std::ceil(r.threshold + 8.5 * r.scale)) + sh;
+        top = std::max(top, std::min<int64_t>(i1, INT32_MAX) + 1);
     }
     // (16 KB: the normal-approximation pass is latency-bound, and a table of
     // 32 KB held it at 5 waves per CU; counts past the table read pi from

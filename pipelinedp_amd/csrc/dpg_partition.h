@@ -685,7 +685,8 @@ __device__ __forceinline__ uint32_t scatter_scan_update(uint32_t *cnt, uint32_t 
                                                         uint32_t *cur, uint32_t F,
                                                         uint32_t *sh16, uint32_t *goff = nullptr,
                                                         uint32_t cap = 0, uint32_t dump = 0,
-                                                        uint32_t *err = nullptr) {
+                                                        uint32_t *err = nullptr,
+                                                        const uint32_t *lb = nullptr) {
     constexpr int NW = T / 64;
     const uint32_t d0 = DPT * threadIdx.x;
     uint32_t c[DPT], x = 0;
@@ -737,7 +738,9 @@ __device__ __forceinline__ uint32_t scatter_scan_update(uint32_t *cnt, uint32_t 
                 if (c[u]) {
                     const uint32_t ou = kPair ? o[u] : atomicAdd(&goff[d0 + u], c[u]);
                     if (ou + c[u] <= cap) {
-                        cur[d0 + u] += ou + c[u];
+                        // lb (piece mode): the region bases in LDS, so cur
+                        // needs no reset between sub-tiles
+                        cur[d0 + u] = (lb ? lb[d0 + u] : cur[d0 + u]) + ou + c[u];
                     } else {
                         cur[d0 + u] = dump + e + c[u];
                         atomicOr(err, 16u);
@@ -755,6 +758,77 @@ __device__ __forceinline__ uint32_t scatter_scan_update(uint32_t *cnt, uint32_t 
     if (threadIdx.x == 0) dstart[F] = total;
     __syncthreads();
     return total;
+}
+
+// Piece mode's digit scan with the run reservations consumed late: the
+// two runs of a thread's digit pair are reserved by one 64-bit atomic issued
+// before the scan's barrier, as in scatter_scan_update, but the returned
+// cursors are only needed at the write-out, so the caller stages first and
+// then calls scatter_rsv_finish; the atomic's round trip (and, being younger
+// in the vmcnt order, the drain of the previous write-out's stores) overlaps
+// the staging instead of stalling the scan.
+struct PcRsv {
+    uint32_t c[2];  // the thread's two digit counts
+    uint32_t e0;    // local start of its first digit
+    unsigned long long old;
+};
+__device__ __forceinline__ uint32_t scatter_scan_pc(uint32_t *cnt, uint32_t *dstart, uint32_t F,
+                                                    uint32_t *sh16, uint32_t *goff, PcRsv &r) {
+    const uint32_t d0 = 2 * threadIdx.x;
+    r.c[0] = d0 < F ? cnt[d0] : 0u;
+    r.c[1] = d0 + 1 < F ? cnt[d0 + 1] : 0u;
+    // unconditional (threads past F add 0 to the first pair): a result that
+    // is waited for on one path only is waited for again, with vmcnt(0),
+    // when its register is next overwritten -- after the prefetch loads
+    r.old = atomicAdd(reinterpret_cast<unsigned long long *>(&goff[d0 < F ? d0 : 0u]),
+                      (unsigned long long)r.c[0] | ((unsigned long long)r.c[1] << 32));
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t wt;
+    uint32_t e = wave_excl_scan(r.c[0] + r.c[1], wt);
+    if (lane == 63) sh16[w] = wt;
+    __syncthreads();
+    uint32_t total = 0;
+#pragma unroll
+    for (int k = 0; k < kScatThreads / 64; ++k) {
+        const uint32_t y = sh16[k];
+        if (k < w) e += y;
+        total += y;
+    }
+    r.e0 = e;
+    if (d0 < F) {
+        dstart[d0] = e;
+        cnt[d0] = 0;
+    }
+    if (d0 + 1 < F) {
+        dstart[d0 + 1] = e + r.c[0];
+        cnt[d0 + 1] = 0;
+    }
+    if (threadIdx.x == 0) dstart[F] = total;
+    __syncthreads();
+    return total;
+}
+// cur[d] of the thread's two digits from the reservation (lb: the regions'
+// bases); a run past the region's capacity goes to the dump area and raises
+// err bit 16.  The caller's next barrier publishes cur.
+__device__ __forceinline__ void scatter_rsv_finish(const PcRsv &r, uint32_t *cur, const uint32_t *lb,
+                                                   uint32_t F, uint32_t cap, uint32_t dump,
+                                                   uint32_t *err) {
+    const uint32_t d0 = 2 * threadIdx.x;
+    // the returned cursors are consumed on every path (see scatter_scan_pc)
+    const uint32_t o[2] = {(uint32_t)r.old, (uint32_t)(r.old >> 32)};
+    uint32_t e = r.e0;
+    bool over = false;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const bool fits = o[u] + r.c[u] <= cap;
+        const uint32_t v = fits ? (lb[d0 + u < F ? d0 + u : 0u] + o[u] + r.c[u]) : dump + e + r.c[u];
+        if (d0 + u < F && r.c[u]) {
+            cur[d0 + u] = v;
+            over = over || !fits;
+        }
+        e += r.c[u];
+    }
+    if (over) atomicOr(err, 16u);
 }
 
 // grid S: base[s][d] = seg_start[s] + exclusive_prefix_d(tot[s][.])  (F <= 4096)
@@ -844,6 +918,12 @@ constexpr size_t scatter_lds_core() {
 // next sub-tile's prefetched loads (level 1 has one sub-tile per tile).
 #ifndef DPG_SCAT_LBASE
 #define DPG_SCAT_LBASE 1
+#endif
+#ifndef DPG_PC_NORESET
+#define DPG_PC_NORESET 1
+#endif
+#ifndef DPG_PC_LATE_RSV
+#define DPG_PC_LATE_RSV 1
 #endif
 template <class Src, class Rec, int IPT, int FMAX>
 constexpr bool scatter_lbase() {
@@ -981,24 +1061,40 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
     uint64_t slast = __builtin_amdgcn_s_memtime();
 #endif
     TileDesc td = uniform_tile(tiles, t);
+    // piece mode: the end of the input (the last tile's end)
+    const int64_t n_end = kPc ? uniform_tile(tiles, nt - 1).end : 0;
     load_sub(td.begin, (uint32_t)min<int64_t>(SUB, td.end - td.begin));
+    // piece mode with the region bases in LDS: cur is assigned (not
+    // accumulated) by the digit scan and cnt is zeroed there, so the tiles
+    // need no reset between them -- one setup here.  The per-tile reset was
+    // a loop whose spilled LDS address (scratch reload, s_waitcnt vmcnt(0))
+    // drained the previous write-out's stores and the prefetched loads at
+    // every tile transition.
+    constexpr bool kPcLB = kPc && kLB && DPG_PC_NORESET;
+    if constexpr (kPcLB) {
+        for (uint32_t d = tid; d < F; d += kScatThreads) {
+            lbase[d] = (uint32_t)base[(size_t)(blockIdx.x & 7u) * F + d];
+            cnt[d] = 0;
+        }
+        __syncthreads();
+    }
     for (;;) {
     // the next tile's queue slot: one atomic by thread 0, issued now,
     // published in LDS with the first ranking barrier below
     uint32_t nq = 0;
+    const uint32_t *cb = nullptr;
+    uint32_t *gof = goff ? goff + (size_t)(kPc ? (blockIdx.x & 7u) : td.pad) * F : nullptr;
+    if constexpr (!kPcLB) {
     if (xq.q && tid == 0) nq = atomicAdd(&xq.next[xq_id], 1u);
     __syncthreads();   // the previous tile's write-out has read cur / dstart / sh_next
     // chunked tile scan: the tile's offset is relative to its chunk
-    const uint32_t *cb = nullptr;
     if (cbase) {
         const uint32_t nta = seg_ntiles[td.seg], per = (nta + C - 1) / C;
         cb = cbase + ((size_t)td.seg * C + (t - seg_tile_base[td.seg]) / per) * F;
     }
     // grouped mode: the work item is one sub-tile of group td.pad, whose runs
     // are reserved at the digit scan
-    const uint32_t gsel = kPc ? (blockIdx.x & 7u) : td.pad;
     const uint32_t bsel = kPc ? (blockIdx.x & 7u) : td.seg;
-    uint32_t *gof = goff ? goff + (size_t)gsel * F : nullptr;
     if (kLB && goff) {
         // a thread reads back only the lbase entries it wrote itself
         if (bsel != lseg) {
@@ -1017,6 +1113,7 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
         }
     }
     __syncthreads();
+    }  // !kPcLB
     uint32_t tn = kNone;
     TileDesc tdn = td;
     DPG_SCAT_MARK(4);
@@ -1057,8 +1154,14 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
         if (xq.q && tid == 0 && sb == td.begin) sh_next = nq;
         __syncthreads();
         DPG_SCAT_MARK(0);
-        const uint32_t total = scatter_scan_update<kScatThreads, FMAX / kScatThreads, kPc>(
-            cnt, dstart, cur, F, sh16, gof, pcap, pdump, perr);
+        constexpr bool kLate = kPcLB && FMAX == 2 * kScatThreads && DPG_PC_LATE_RSV;
+        PcRsv rsv;
+        uint32_t total;
+        if constexpr (kLate)
+            total = scatter_scan_pc(cnt, dstart, F, sh16, gof, rsv);
+        else
+            total = scatter_scan_update<kScatThreads, FMAX / kScatThreads, kPc>(
+                cnt, dstart, cur, F, sh16, gof, pcap, pdump, perr, kPcLB ? lbase : nullptr);
         DPG_SCAT_MARK(1);
         {
             uint32_t ds[IPT];
@@ -1071,6 +1174,7 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
                 if constexpr (kSD) sdig[pos] = (uint16_t)(dr[j] & 0xFFFu);
             }
         }
+        if constexpr (kLate) scatter_rsv_finish(rsv, cur, lbase, F, pcap, pdump, perr);
         __syncthreads();
         DPG_SCAT_MARK(2);
         const int64_t nb = sb + SUB;
@@ -1083,7 +1187,11 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
             if constexpr (HasTilePrefetch<Src>::value && kPc) {
                 if (nlim == 0 && it + gridDim.x < nt) {
                     tn = it + gridDim.x;
-                    tdn = uniform_tile(tiles, tn);
+                    // one-sub-tile tiles cut evenly (k_build_tiles_single):
+                    // computed, not loaded (a descriptor load here waited
+                    // with vmcnt(0) on the critical path of every sub-tile)
+                    tdn.begin = (int64_t)tn * SUB;
+                    tdn.end = min(tdn.begin + SUB, n_end);
                     lb = tdn.begin;
                     ll = (uint32_t)min<int64_t>(SUB, tdn.end - tdn.begin);
                 }
@@ -1104,7 +1212,12 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
         // slots past the end repeat the last staged record, whose store they
         // duplicate (same value, same address)
         constexpr int WB = IPT < DPG_SCAT_WB ? IPT : DPG_SCAT_WB;
-        for (uint32_t k0 = 0; k0 < total; k0 += WB * kScatThreads) {
+        // piece mode: a fixed trip count, fully unrolled -- as a loop, the
+        // compiler's loop-preheader vmcnt flush (a loop with stores, no loads,
+        // using a register it still counts as loaded outside) waited for the
+        // prefetched loads just issued before the first store
+        constexpr int kWbIter = (IPT + WB - 1) / WB;
+        auto write_batch = [&](uint32_t k0) {
             W x[WB];
             uint32_t dd[WB], kc[WB];
 #pragma unroll
@@ -1126,8 +1239,8 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
             // cur already includes this sub-tile: its run ends at cur[d]
             // (non-temporal loads / stores measured slower: the partial
             // lines of the runs merge in L2)
-#pragma unroll
 #if DPG_EXP_SCAT_NOSTORE  // diagnostic only (wrong results): the scatter without its stores
+#pragma unroll
             for (int u = 0; u < WB; ++u) {
                 uint32_t w0;
                 __builtin_memcpy(&w0, &x[u], 4);
@@ -1135,8 +1248,18 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
                     *reinterpret_cast<W *>(&out[c1[u] - c2[u] + kc[u]]) = x[u];
             }
 #else
+#pragma unroll
             for (int u = 0; u < WB; ++u) *reinterpret_cast<W *>(&out[c1[u] - c2[u] + kc[u]]) = x[u];
 #endif
+        };
+        if constexpr (kPc) {
+#pragma unroll
+            for (int b = 0; b < kWbIter; ++b) {
+                if ((uint32_t)b * WB * kScatThreads >= total) break;
+                write_batch((uint32_t)b * WB * kScatThreads);
+            }
+        } else {
+            for (uint32_t k0 = 0; k0 < total; k0 += WB * kScatThreads) write_batch(k0);
         }
         // the next sub-tile's first barrier (after its ranking) orders this
         // write-out's LDS reads before the next scan and staging

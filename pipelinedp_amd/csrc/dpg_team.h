@@ -86,13 +86,20 @@ __device__ __forceinline__ bool team_barrier(const TeamSync &ts, uint32_t team, 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's reservations / zeroing done
     __syncthreads();
     uint32_t *ctr = ts.arrive + team * kTeamArriveStride;
-    if (threadIdx.x == 0)
+    // the first poll is issued before `between`: vmcnt counts in issue order,
+    // so a poll issued after the prefetch loads would wait for all of them
+    // (wave 0 then held the whole workgroup at the closing barrier for the
+    // next share's load latency although the team had long arrived)
+    uint32_t seen = 0;
+    if (threadIdx.x == 0) {
         __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        seen = ld_agent(ctr);
+    }
     between();
     if (threadIdx.x == 0) {
         const uint64_t t0 = wall_clock64();
         uint32_t ok = 1;
-        while (ld_agent(ctr) < target) {
+        for (; seen < target; seen = ld_agent(ctr)) {
             if (ld_agent(ts.abort)) {
                 ok = 0;
                 break;
@@ -115,6 +122,22 @@ __device__ __forceinline__ bool team_barrier(const TeamSync &ts, uint32_t team, 
 // s as 8 pieces, one per XCD region: records [rbase[x F1 + s], + cum[x F1 +
 // s]) for x < 8; tot[s] = their sum, ostart[s] = the bucket's start in the
 // (compact) level-2 output.  Region starts are even (C even).
+// One bucket's pieces in one 128-byte record (k_piece_totals), read by two
+// scalar loads: a team member's next share then costs one round trip of
+// descriptor reads instead of ten dependent ones (bucket size, start, first
+// region, and each piece's region offset and count).
+struct PieceDesc {
+    uint32_t n;        // padded records (each piece rounded up to even)
+    uint32_t pad0;
+    int64_t ostart;    // the bucket's start in the compact level-2 output
+    int64_t base0;     // the bucket's first region (rbase[s])
+    uint32_t ppre[8];  // padded exclusive prefix of the pieces
+    uint32_t dl[8];    // index i of piece p sits at base0 + i + dl[p] (mod 2^32)
+    uint32_t cend[8];  // end of piece p's records in the padded index space
+    uint32_t pad1[2];
+};
+static_assert(sizeof(PieceDesc) == 128, "PieceDesc is two 64-byte scalar loads");
+
 struct PieceTab {
     const int64_t *rbase;
     const uint32_t *cum;
@@ -122,7 +145,18 @@ struct PieceTab {
     const uint32_t *ptot;  // the pieces' counts each rounded up to even, summed
     const int64_t *ostart;
     uint32_t F1;
+    const PieceDesc *desc = nullptr;  // [F1]
 };
+
+typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+// 128 bytes at a uniform, 64-byte aligned address into scalar registers
+// (loads only: nothing is written through the scalar cache)
+__device__ __forceinline__ void sload_desc(const PieceDesc *p, u32x16 &a, u32x16 &b) {
+    asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx16 %1, %2, 0x40\n\ts_waitcnt lgkmcnt(0)"
+                 : "=s"(a), "=s"(b)
+                 : "s"(p)
+                 : "memory");
+}
 
 // Level 2 over S level-1 buckets (seg_start / seg_cnt; every count <= T *
 // kTeamSub, checked by the host): records of bucket s land in out[seg_start[s],
@@ -244,6 +278,42 @@ __global__ __launch_bounds__(kScatThreads) void k_part2_team(SrcAoS<R> src,
         }
         vmask = vm;
     };
+    // the same from the bucket's PieceDesc, already in scalar registers
+    auto load_pieces_desc = [&](const u32x16 &da, const u32x16 &db, uint32_t b0, uint32_t lim) {
+        const int64_t base0 = (int64_t)(((uint64_t)da[5] << 32) | da[4]);
+        uint32_t ppre[8], dl[8], ce[8];
+#pragma unroll
+        for (int p = 0; p < 8; ++p) {
+            ppre[p] = da[6 + p];
+            dl[p] = p < 2 ? da[14 + p] : db[p - 2];
+            ce[p] = db[6 + p];
+        }
+        const char *bp = reinterpret_cast<const char *>(src.a + base0);
+        uint32_t vm = 0;
+#pragma unroll
+        for (int mm = 0; mm < IPT / 2; ++mm) {
+            const uint32_t o = mm * 2 * kScatThreads + 2 * tid;
+            const uint32_t i = b0 + min(o, lim - 2);  // even (b0, lim even)
+            uint32_t d = dl[0], c = ce[0];
+#pragma unroll
+            for (int p = 1; p < 8; ++p) {
+                const bool in = i >= ppre[p];
+                d = in ? dl[p] : d;
+                c = in ? ce[p] : c;
+            }
+            R x0, x1;
+            const uint32_t boff = (i + d) * (uint32_t)sizeof(R);
+            const u64x2 w = *reinterpret_cast<const u64x2 *>(bp + boff);
+            const uint64_t w0 = w.x, w1 = w.y;
+            __builtin_memcpy(&x0, &w0, sizeof(R));
+            __builtin_memcpy(&x1, &w1, sizeof(R));
+            rec[2 * mm] = x0;
+            rec[2 * mm + 1] = x1;
+            vm |= (i < c ? 1u : 0u) << (2 * mm);
+            vm |= (i + 1 < c ? 1u : 0u) << (2 * mm + 1);
+        }
+        vmask = vm;
+    };
     uint32_t k = 0;  // buckets done = team barriers passed
     // kPF: the share of this member's next non-empty bucket (piece mode: its
     // piece descriptors too) is loaded during the current bucket's team
@@ -256,27 +326,59 @@ __global__ __launch_bounds__(kScatThreads) void k_part2_team(SrcAoS<R> src,
             if (__builtin_amdgcn_readfirstlane(kPc ? pt.ptot[s] : seg_cnt[s]) != 0) break;
         return s;
     };
-    // the loads of one share (piece mode: its 8-piece descriptors first)
+    // the loads of one share (piece mode: its 8-piece descriptors first);
+    // the share's bounds are kept for the bucket's iteration (kPF), whose
+    // loop head then issues no loads: a load there waited with vmcnt(0) for
+    // the previous bucket's write-out stores before the ranking could start
+    int64_t pf_st = 0;
+    uint32_t pf_n = 0, pf_b0 = 0, pf_lim = 0;
+    constexpr bool use_desc = kPc && kPF;  // the host always builds pt.desc
     auto load_share = [&](uint32_t s) {
-        int64_t st;
-        uint32_t n, b0, lim;
-        share(s, st, n, b0, lim);
+        if constexpr (kPc) {
+            if constexpr (use_desc) {
+                // branch-free: past the last bucket (s = S) the loads read the
+                // last one, a member past the bucket's end reads its tail
+                // (inside the regions, masked out): no path without loads,
+                // so the barrier's first poll is waited for by count
+                u32x16 da, db;
+                sload_desc(pt.desc + min(s, S - 1), da, db);
+                pf_n = da[0];
+                pf_st = (int64_t)(((uint64_t)da[3] << 32) | da[2]);
+                const uint32_t q = ((pf_n + T - 1) / T + 1) & ~1u;
+                pf_b0 = min(pf_n, m * q);
+                pf_lim = min(pf_n, pf_b0 + q) - pf_b0;
+                load_pieces_desc(da, db, pf_b0, max(pf_lim, 2u));
+                return;
+            }
+        }
+        share(s, pf_st, pf_n, pf_b0, pf_lim);
         if constexpr (kPc) {
             vmask = 0;
-            if (lim > 0) load_pieces(s, b0, lim);
+            if (pf_lim > 0) load_pieces(s, pf_b0, pf_lim);
         } else {
-            load(st + b0, lim);
+            load(pf_st + pf_b0, pf_lim);
         }
     };
     uint32_t pf_s = S;
     if constexpr (kPF) {
         pf_s = next_nonempty(team);
-        if (pf_s < S) load_share(pf_s);
+        if (use_desc || pf_s < S) load_share(pf_s);
     }
     for (uint32_t s = team; s < S; s += 8) {
         int64_t st;
         uint32_t n, b0, lim;
-        share(s, st, n, b0, lim);
+        if constexpr (kPF) {
+            if (s == pf_s) {
+                st = pf_st;
+                n = pf_n;
+                b0 = pf_b0;
+                lim = pf_lim;
+            } else {
+                share(s, st, n, b0, lim);  // an empty bucket (next_nonempty skipped it)
+            }
+        } else {
+            share(s, st, n, b0, lim);
+        }
         if (n == 0) {
             if (m == 0)
                 for (uint32_t d = tid; d < F2; d += kScatThreads) {
@@ -335,26 +437,29 @@ __global__ __launch_bounds__(kScatThreads) void k_part2_team(SrcAoS<R> src,
 #pragma unroll
             for (int u = 0; u < DPT; ++u) {
                 dstart[d0 + u] = e;
-                cur[d0 + u] = o[u];
+                if constexpr (!kPF) cur[d0 + u] = o[u];
                 cnt[d0 + u] = 0;
                 e += c[u];
             }
             if (tid == 0) dstart[F] = nv;
+            if constexpr (kPF) {
+                // ---- stage by local digit now (independent of the team
+                // totals); the reservations' round trip overlaps it
+                __syncthreads();
+#pragma unroll
+                for (int j = 0; j < IPT; ++j) {
+                    const uint32_t pos = dr[j] != ~0u ? dstart[dr[j] & 0xFFFu] + (dr[j] >> 12) : (uint32_t)SUB;
+                    stage[pos] = to_words(rec[j]);
+                }
+#pragma unroll
+                for (int u = 0; u < DPT; ++u) cur[d0 + u] = o[u];
+                pf_s = next_nonempty(s + 8);
+            }
         }
         ++k;
-        if constexpr (kPF) {
-            // ---- stage by local digit now (independent of the team totals)
-            __syncthreads();
-#pragma unroll
-            for (int j = 0; j < IPT; ++j) {
-                const uint32_t pos = dr[j] != ~0u ? dstart[dr[j] & 0xFFFu] + (dr[j] >> 12) : (uint32_t)SUB;
-                stage[pos] = to_words(rec[j]);
-            }
-            pf_s = next_nonempty(s + 8);
-        }
         auto prefetch = [&]() {
             if constexpr (kPF) {
-                if (pf_s < S) load_share(pf_s);
+                if (use_desc || pf_s < S) load_share(pf_s);
             }
         };
         if (!team_barrier(ts, team, T * k, &sh_ok, prefetch)) return;

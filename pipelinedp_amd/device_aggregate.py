@@ -16,6 +16,7 @@ Device pipeline per call (include/dpg.h):
 """
 import ctypes
 import os
+import warnings
 from typing import Optional, Sequence
 
 import numpy as np
@@ -35,6 +36,28 @@ _SYNC_COMPACT = os.environ.get("DPG_SYNC_COMPACT", "0") == "1"
 
 def _ptr(t: Optional[torch.Tensor]):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+# Results dropped before their device info word was read: their
+# bounding error bits are checked when the release has finished, at the
+# latest by the next release on any backend, and reported as a warning.
+_DROPPED = []
+
+
+def check_dropped(block: bool = False) -> None:
+    """Warns about dropped, never-read results whose bounding latched an
+    internal error; block=True waits for the unfinished ones."""
+    keep = []
+    for info, ev in _DROPPED:
+        if ev is not None and not block and not ev.query():
+            keep.append((info, ev))
+            continue
+        if ev is not None:
+            ev.synchronize()
+        if int(info[1].item()) & 2:
+            warnings.warn("a DeviceResult dropped without being read had an internal bounding "
+                          "error (hash-table overflow); its release was invalid", RuntimeWarning)
+    _DROPPED[:] = keep
 
 
 class DeviceResult:
@@ -67,15 +90,26 @@ class DeviceResult:
             self._pending[4].synchronize()
         k, err = (int(x) for x in info.tolist())
         if err & 2:
+            self._pending = None  # reported here, not again when dropped
             raise _native.NativeError(
                 "dpg_compact_kept failed (HIP error): internal hash-table error in bounding")
         ids = self._ids[:k]
         if stride != 1 or offset:  # several ranks: this rank's slice
             ids = ids * stride + offset
-        self._ids = ids
-        self._vals = (self._vals[:k * n_out].view(k, n_out) if n_out
-                      else torch.empty((k, 0), dtype=torch.float64, device=self._vals.device))
+        vals = (self._vals[:k * n_out].view(k, n_out) if n_out
+                else torch.empty((k, 0), dtype=torch.float64, device=self._vals.device))
+        # a small kept set does not pin the partition-sized compaction
+        # buffers: compact copies
+        if 2 * k < self._ids.numel():
+            ids = ids.clone() if ids.data_ptr() == self._ids.data_ptr() else ids
+            vals = vals.clone()
+        self._ids, self._vals = ids, vals
         self._pending = None
+
+    def __del__(self):
+        p = getattr(self, "_pending", None)
+        if p is not None:
+            _DROPPED.append((p[0], p[4] if len(p) > 4 else None))
 
     @property
     def partition_ids(self) -> torch.Tensor:
@@ -198,6 +232,8 @@ class DeviceAggregation:
         return self.nonce, nnz_bound
 
     def _run(self, gather: bool) -> DeviceResult:
+        if _DROPPED:
+            check_dropped()
         backend = self.backend
         ctx = backend.ctx
         dev = backend.device

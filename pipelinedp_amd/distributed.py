@@ -47,6 +47,8 @@ import torch
 import torch.distributed as dist
 
 _PACK_ORDER = ("rows", "count", "sum", "nsum", "nsq")
+_PACK_DTYPE = {"rows": torch.int64, "count": torch.int64, "sum": torch.float64,
+               "nsum": torch.float64, "nsq": torch.float64}
 _I64_MIN = -(1 << 63)
 
 
@@ -134,7 +136,13 @@ def reduce_scatter_partials(tensors: Dict[str, Optional[torch.Tensor]], P: int, 
     names = _names(tensors)
     A = len(names)
     dev = tensors[names[0]].device
-    fused = ctx is not None and dev.type == "cuda"
+    # the library's pack / unpack kernels read and write the partials
+    # through raw pointers: only contiguous arrays of the layout they assume
+    # (int64 rows / count, float64 sums) take them; anything else takes the
+    # torch path, which handles any dtype
+    fused = (ctx is not None and dev.type == "cuda" and
+             all(tensors[k].is_contiguous() and tensors[k].dtype == _PACK_DTYPE[k]
+                 and tensors[k].numel() >= P for k in names))
     pack = torch.empty((world, A * S + 1), dtype=torch.float64, device=dev)
     if fused:
         from pipelinedp_amd import _native

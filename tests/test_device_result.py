@@ -54,3 +54,39 @@ def test_latched_internal_error_raises_on_first_use():
 def test_resolved_result_passes_through():
     r = DeviceResult(torch.tensor([5, 7]), torch.ones(2, 1, dtype=torch.float64), ("count",), None)
     assert r.partition_ids.tolist() == [5, 7] and r.values.shape == (2, 1)
+
+
+def test_small_kept_set_is_copied_out_of_the_full_buffers():
+    ids, vals = _full(2, 1, cap=10)
+    r = DeviceResult(ids, vals, ("count",), None, pending=(torch.tensor([2, 0]), 1, 1, 0))
+    got = r.partition_ids
+    assert got.tolist() == [0, 3]
+    assert got.data_ptr() != ids.data_ptr() and r.values.data_ptr() != vals.data_ptr()
+    # a kept set of more than half the buffer stays a view
+    ids, vals = _full(8, 1, cap=10)
+    r = DeviceResult(ids, vals, ("count",), None, pending=(torch.tensor([8, 0]), 1, 1, 0))
+    assert r.partition_ids.data_ptr() == ids.data_ptr()
+
+
+def test_dropped_unread_result_with_error_warns_at_check():
+    from pipelinedp_amd import device_aggregate as da
+    da._DROPPED.clear()
+    ids, vals = _full(2, 1)
+    r = DeviceResult(ids, vals, ("count",), None, pending=(torch.tensor([2, 2]), 1, 1, 0))
+    del r
+    assert len(da._DROPPED) == 1
+    with pytest.warns(RuntimeWarning, match="dropped"):
+        da.check_dropped(block=True)
+    assert not da._DROPPED
+    # a clean dropped result is checked silently; a read one is not queued
+    r = DeviceResult(ids, vals, ("count",), None, pending=(torch.tensor([2, 0]), 1, 1, 0))
+    del r
+    r2 = DeviceResult(ids, vals, ("count",), None, pending=(torch.tensor([2, 0]), 1, 1, 0))
+    r2.partition_ids
+    del r2
+    assert len(da._DROPPED) == 1
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        da.check_dropped(block=True)
+    assert not da._DROPPED

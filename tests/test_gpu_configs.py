@@ -116,6 +116,7 @@ def test_config2_level2_paths_match_oracle(built, config2_data, monkeypatch, mod
                        else "0")
     if mode == "team_abort":
         monkeypatch.setenv("DPG_DEBUG_TEAM_ABORT", "1")
+        monkeypatch.setenv("DPG_DEBUG_TEAM_BACKOFF", "1")
     if mode == "piece_overflow":
         monkeypatch.setenv("DPG_DEBUG_PIECE_CAP", "64")
     pid, pk, val = config2_data
@@ -129,23 +130,27 @@ def test_config2_level2_paths_match_oracle(built, config2_data, monkeypatch, mod
     assert ("partition2:hist" in stages) == (mode in ("grouped", "team_abort"))
     assert ("partition2:team_redo" in stages) == (mode == "team_abort")
     if mode == "team_abort":
-        # the timeout is sticky on the context: the next release on the same
-        # backend takes the histogram level 2 directly, and
-        # still matches the oracle
+        # the timeout backs off on the context: the next
+        # release on the same backend (back-off of 1 call, test hook
+        # DPG_DEBUG_TEAM_BACKOFF; 64 calls by default) takes the histogram
+        # level 2 directly and says so in its stage times; the one after
+        # tries the team path again; both still match the oracle
         monkeypatch.delenv("DPG_DEBUG_TEAM_ABORT")
-        acc = pdp.NaiveBudgetAccountant(1.0, 1e-6)
         cols = pdp.ColumnarData(pid=torch.from_numpy(pid).cuda(), pk=torch.from_numpy(pk).cuda(),
                                 value=torch.from_numpy(val).cuda(), n_partitions=P2)
-        res2 = pdp.DPEngine(acc, res.backend).aggregate(
-            cols, _c2_params(8, 2), pdp.DataExtractors("pid", "pk", "value"))
-        acc.compute_budgets()
-        res2.noise_enabled = False
-        res2.nonce = 1234
-        res2.materialize()
-        got2 = {k: v.cpu().numpy() for k, v in res2.last_partials.items() if v is not None}
-        _assert_partials(got2, ref)
-        stages2 = res.backend.ctx.stage_times()
-        assert "partition2:team" not in stages2 and "partition2:hist" in stages2
+        for again in (False, True):
+            acc = pdp.NaiveBudgetAccountant(1.0, 1e-6)
+            res2 = pdp.DPEngine(acc, res.backend).aggregate(
+                cols, _c2_params(8, 2), pdp.DataExtractors("pid", "pk", "value"))
+            acc.compute_budgets()
+            res2.noise_enabled = False
+            res2.nonce = 1234
+            res2.materialize()
+            got2 = {k: v.cpu().numpy() for k, v in res2.last_partials.items() if v is not None}
+            _assert_partials(got2, ref)
+            stages2 = res.backend.ctx.stage_times()
+            assert ("partition2:team" in stages2) == again
+            assert ("team_backoff" in stages2) == (not again)
 
 
 def test_config2_pieces_range_error(built, config2_data, monkeypatch):
