@@ -585,7 +585,9 @@ def main():
     kept_recs = int(lp["count"].sum().item())
     stage_ms = dict(stage_tot)
     path_ms = sum(v for k, v in stage_ms.items() if k != "bounding")
-    algo_bytes = ALGO_BYTES_PER_RECORD * args.records
+    # 24 B per record; MEAN+VARIANCE (config 4) adds 40 B per
+    # partition of partials (rows, count, nsum, nsq + the noised outputs)
+    algo_bytes = ALGO_BYTES_PER_RECORD * args.records + (40 * P if c4 else 0)
     # record / item formats of the two workloads: config
     # 4 packs 12-byte R12 records (70 key bits) and 24-byte ItemV items
     # (MEAN + VARIANCE without SUM: rows, count, nsum, nsq partials)
@@ -643,7 +645,9 @@ def main():
                      "traffic": (tj["bytes_per_step"] if tj else None),
                      "kernel": "whole path (dpg_bound_aggregate + select/noise + compact)",
                      "device_ms": dev_ms_max,
-                     "note": "achieved = 24 B/record x records / device time per step (HIP "
+                     "algorithmic_bytes": algo_bytes,
+                     "note": "achieved = 24 B/record x records (+ 40 B/partition for MEAN+VARIANCE, "
+                             "SURVEY.md 8(d)) / device time per step (HIP "
                              "events on the kernels' stream, max over ranks); traffic = PMC "
                              "HBM bytes per step (FETCH_SIZE x calibrated factor + WRITE_SIZE) "
                              f"from {tsrc}"},

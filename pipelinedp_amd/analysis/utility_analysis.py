@@ -277,11 +277,30 @@ class UtilityAnalysis:
         return torch.nonzero(has).flatten()
 
     # ------------------------------------------------ cross-partition combine
-    def _report(self, c: int, v: list) -> metrics.UtilityReport:
-        """UtilityReport of configuration c from its summed fields v (the
-        field layout of dpg_utility_analysis' report output, as a list of
-        Python floats: per-element numpy scalar access dominated the report
-        assembly of a 64-configuration sweep)."""
+    def _scaled(self, rows: np.ndarray) -> np.ndarray:
+        """The report fields of rows [..., F] with every per-partition
+        average already divided out (one vectorised pass instead of ~10
+        Python multiplies per ValueErrors object): the ValueErrors blocks
+        times 1 / (total weight), the DataDropInfo fields times 1 / (the
+        metric's total); IEEE products, identical to the scalar form."""
+        out = rows.copy()
+        with np.errstate(divide="ignore"):
+            tw = rows[..., 1]
+            ws = np.where(tw == 0, 0.0, 1.0 / np.where(tw == 0, 1.0, tw))
+            for mi in range(len(self.metrics)):
+                b = 4 + 24 * mi
+                tot = rows[..., b]
+                ds = np.where(tot == 0, 1.0, 1.0 / np.where(tot == 0, 1.0, tot))
+                out[..., b + 1:b + 4] *= ds[..., None]
+                out[..., b + 4:b + 24] *= ws[..., None]
+        return out
+
+    def _report(self, c: int, v: list, sc: list) -> metrics.UtilityReport:
+        """UtilityReport of configuration c from its summed fields v and
+        their scaled form sc (_scaled), both the field layout of
+        dpg_utility_analysis' report output as lists of Python floats
+        (per-element numpy scalar access dominated the report assembly of a
+        64-configuration sweep)."""
         # positional construction throughout (fields in declaration order,
         # metrics.py): keyword matching was half of the assembly time of a
         # 64-configuration report set
@@ -297,29 +316,21 @@ class UtilityAnalysis:
         report = metrics.UtilityReport(c, info)
         if not self.metrics:
             return report
-        total_w = v[1]
-        wscale = 0.0 if total_w == 0 else 1.0 / total_w
         errs = []
-        cf = self.configs[c]
-        noise_kind = cf.params.noise_kind
-
+        noise_kind = self.configs[c].params.noise_kind
         VE, CBE, MV = metrics.ValueErrors, metrics.ContributionBoundingErrors, metrics.MeanVariance
-
-        def verr(b):  # ValueErrors from the 10 weighted sums at v[b:b + 10]
-            w = wscale
-            return VE(CBE(MV(v[b] * w, v[b + 1] * w), v[b + 2] * w, v[b + 3] * w),
-                      v[b + 4] * w, v[b + 5] * w, v[b + 6] * w, v[b + 7] * w, v[b + 8] * w,
-                      v[b + 9] * w)
+        MU, DDI = metrics.MetricUtility, metrics.DataDropInfo
         # the reference labels metric_errors by zipping them with the user's
         # metric order (cross_partition_combiners.py:208-212)
-        for mi, (m, um, std) in enumerate(zip(self.metrics, self._user_metrics, cf.std_list)):
+        for mi, (um, std) in enumerate(zip(self._user_metrics, self.configs[c].std_list)):
             b = 4 + 24 * mi
-            tot = v[b]
-            dscale = 1.0 if tot == 0 else 1.0 / tot
-            errs.append(metrics.MetricUtility(
-                um, std, noise_kind,
-                metrics.DataDropInfo(v[b + 1] * dscale, v[b + 2] * dscale, v[b + 3] * dscale),
-                verr(b + 4), verr(b + 14)))
+            a, r = b + 4, b + 14
+            errs.append(MU(
+                um, std, noise_kind, DDI(sc[b + 1], sc[b + 2], sc[b + 3]),
+                VE(CBE(MV(sc[a], sc[a + 1]), sc[a + 2], sc[a + 3]), sc[a + 4], sc[a + 5],
+                   sc[a + 6], sc[a + 7], sc[a + 8], sc[a + 9]),
+                VE(CBE(MV(sc[r], sc[r + 1]), sc[r + 2], sc[r + 3]), sc[r + 4], sc[r + 5],
+                   sc[r + 6], sc[r + 7], sc[r + 8], sc[r + 9])))
         report.metric_errors = errs
         return report
 
@@ -330,12 +341,15 @@ class UtilityAnalysis:
         self.run()
         byb = self.rep.permute(0, 2, 1).cpu().numpy()        # [bucket, C, F]
         present = np.nonzero(byb[:, 0, 0] > 0)[0].tolist()
-        tot = byb.sum(axis=0).tolist()                        # [C][F]
-        rows = {bi: byb[bi].tolist() for bi in present}       # bucket -> [C][F]
+        # totals and the present buckets as one [1 + buckets, C, F] block
+        block = np.concatenate([byb.sum(axis=0)[None], byb[present]], axis=0)
+        raw = block.tolist()
+        scaled = self._scaled(block).tolist()
         self._user_metrics = list(self.options.aggregate_params.metrics)
         for cf in self.configs:
             cf.std_list = [cf.noise_std[m] for m in self.metrics]
-        bins = [(bi, BUCKET_BOUNDS[bi], _get_upper_bound(BUCKET_BOUNDS[bi])) for bi in present]
+        bins = [(j + 1, BUCKET_BOUNDS[bi], _get_upper_bound(BUCKET_BOUNDS[bi]))
+                for j, bi in enumerate(present)]
         out = []
         # tens of thousands of small result objects: a generational collection
         # triggered midway scans the whole process heap (~60 ms measured on the
@@ -343,10 +357,10 @@ class UtilityAnalysis:
         gc_on = gc.isenabled()
         gc.disable()
         try:
+            Bin = metrics.UtilityReportBin
             for c in range(len(self.configs)):
-                rep = self._report(c, tot[c])
-                hist = [metrics.UtilityReportBin(lo, hi, self._report(c, rows[bi][c]))
-                        for bi, lo, hi in bins]
+                rep = self._report(c, raw[0][c], scaled[0][c])
+                hist = [Bin(lo, hi, self._report(c, raw[j][c], scaled[j][c])) for j, lo, hi in bins]
                 rep.utility_report_histogram = hist if hist else None
                 out.append(rep)
         finally:

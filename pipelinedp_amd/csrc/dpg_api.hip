@@ -83,10 +83,23 @@ constexpr uint32_t kBucketTarget = 256;  // average records per fine bucket
 // level 2 (records) may take 12 bits (4096 digits: its scatter stages fewer
 // records per sub-tile); refine and item levels keep <= 11
 constexpr uint32_t kMaxB1 = 11, kMaxB2 = 12, kMaxBR = 11;
+// 23-bit plans of 8-byte records (N > 2^30): level 1 takes 12 bits so that
+// level 2 (11 bits) runs by teams (dpg_team.h handles <= 2048 digits); the
+// record then also drops one more stored hash bit, which keeps N up to 2^31
+// in 8-byte records (config 3's 2e9-record shards)
+constexpr uint32_t kMaxB1W = 12;
+// records per thread of the 4096-digit level-1 scatters (LDS: the digit
+// arrays take 48 KB + 16 KB of bases)
+constexpr int kIptL1W = 8;
+// pinned host words: up to 4096 level-1 bucket totals, then the error word
+constexpr uint32_t kPinErr = 4096;
 constexpr uint32_t kChunkGroup = 32;     // fine buckets per packing thread
 // Status of bound_and_reduce when a team level-2 barrier timed out (err bit
 // 8): the caller redoes level 2 with the histogram path.
 constexpr int kRedoLevel2 = -100;
+#ifndef DPG_PC_HALF
+#define DPG_PC_HALF 0
+#endif
 #ifndef DPG_IPT_PC
 #define DPG_IPT_PC 9  // records per thread of the histogram-free level 1 (10 spills: the spill reload waits for the run reservation right after issuing it)
 #endif
@@ -1178,10 +1191,11 @@ __global__ __launch_bounds__(1024) void k_piece_totals(const uint32_t *cum, cons
                                                        uint32_t F, uint32_t *tot, uint32_t *ptot,
                                                        int64_t *ostart, PieceDesc *desc) {
     __shared__ uint32_t sh[16];
-    const uint32_t d0 = 2 * threadIdx.x;
-    uint32_t c[2], x = 0;
+    constexpr int DPT = 4;  // F <= 4096
+    const uint32_t d0 = DPT * threadIdx.x;
+    uint32_t c[DPT], x = 0;
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < DPT; ++u) {
         c[u] = 0;
         uint32_t cp = 0;  // padded: each piece rounded up to even (team pair loads)
         if (d0 + u < F) {
@@ -1205,7 +1219,7 @@ __global__ __launch_bounds__(1024) void k_piece_totals(const uint32_t *cum, cons
     uint32_t total;
     uint32_t e = block_excl_scan_1024(x, sh, total);
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < DPT; ++u) {
         if (d0 + u < F) {
             tot[d0 + u] = c[u];
             ostart[d0 + u] = e;
@@ -1229,12 +1243,12 @@ uint32_t piece_capacity(int64_t n, uint32_t F, int64_t sub) {
     return (uint32_t)c & ~1u;  // even: the team reads pieces by 16-byte pairs
 }
 
-template <class R, int IPT>
+template <class R, int IPT, int FMAX, int NT = kScatThreads>
 int run_level1_pieces(dpg_ctx *ctx, hipStream_t s, const SrcSoAKey<R, true> &src, int64_t n,
                       uint32_t F, uint32_t bits, uint32_t C, R *out, Control *ctl,
                       PieceTab *pt, uint32_t *host_tot) {
     int st = DPG_OK;
-    const int64_t sub = (int64_t)kScatThreads * IPT;
+    const int64_t sub = (int64_t)NT * IPT;
     const uint32_t nt = (uint32_t)((n + sub - 1) / sub);
     WS(tiles, TileDesc, "pieces.tiles", nt);
     WS(stb, uint32_t, "pieces.stb", 1);
@@ -1254,17 +1268,21 @@ int run_level1_pieces(dpg_ctx *ctx, hipStream_t s, const SrcSoAKey<R, true> &src
                                                          &ctl->ntiles[0], XcdQueues{});
     LAUNCH_CHECK();
     using Src = SrcSoAKey<R, true>;
-    constexpr size_t lds = scatter_lds<Src, R, IPT, 2048>();
-    static_assert(lds <= 160 * 1024, "scatter LDS");
-    auto kern = k_scatter<Src, R, IPT, 2048, false>;
+    constexpr size_t lds = scatter_lds<Src, R, IPT, FMAX, NT>();
+    // (kScatThreads / NT) workgroups per CU
+    static_assert(lds <= (size_t)160 * 1024 * NT / kScatThreads - 512, "scatter LDS");
+    if (F > (uint32_t)FMAX) return fail(ctx, DPG_ERR_HIP, "internal: piece level fan-out too large");
+    auto kern = k_scatter<Src, R, IPT, FMAX, false, NT>;
     if (bits <= (uint32_t)agg_bits()) return fail(ctx, DPG_ERR_HIP, "internal: piece level fan-out");
     (void)set_func_attr((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
-    const uint32_t gs = std::min<uint32_t>(nt, (uint32_t)ctx->n_cu);  // one per CU
+    // one 1024-thread workgroup per CU, or two of 512 (whose load, ranking
+    // and write-out phases interleave)
+    const uint32_t gs = std::min<uint32_t>(nt, (uint32_t)ctx->n_cu * (kScatThreads / NT));
     if (int r = scat_phase_begin(ctx, s)) return r;
-    kern<<<gs, kScatThreads, lds, s>>>(src, tiles, &ctl->ntiles[0], F, bits, nullptr, rbase, out,
-                                       XcdQueues{}, nullptr, nullptr, nullptr, 1u, cum, C,
-                                       (uint32_t)((uint64_t)8 * F * C), &ctl->err);
+    kern<<<gs, NT, lds, s>>>(src, tiles, &ctl->ntiles[0], F, bits, nullptr, rbase, out,
+                             XcdQueues{}, nullptr, nullptr, nullptr, 1u, cum, C,
+                             (uint32_t)((uint64_t)8 * F * C), &ctl->err);
     LAUNCH_CHECK();
     if (int r = scat_phase_end(ctx, s, "partition1:pieces", gs)) return r;
     k_piece_totals<<<1, 1024, 0, s>>>(cum, rbase, F, tot, ptot, ostart, pdesc);
@@ -1273,19 +1291,22 @@ int run_level1_pieces(dpg_ctx *ctx, hipStream_t s, const SrcSoAKey<R, true> &src
     if (!ctx->tot_ev && hipEventCreateWithFlags(&ctx->tot_ev, hipEventDisableTiming) != hipSuccess)
         return fail(ctx, DPG_ERR_HIP, "hipEventCreate (totals)");
     HIP_TRY(hipMemcpyAsync(host_tot, tot, (size_t)F * 4, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(host_tot + 4095, &ctl->err, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(host_tot + kPinErr, &ctl->err, 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipEventRecord(ctx->tot_ev, s));
     *pt = PieceTab{rbase, cum, tot, ptot, ostart, F, pdesc};
     return DPG_OK;
 }
 
-// Level 2 by teams of workgroups (dpg_team.h): S level-1 buckets, each
-// <= (n_cu / 8) * kTeamSub records (the caller checked the level-1 totals);
-// pt: the buckets are the pieces of the histogram-free level 1.
+// Level 2 by teams of workgroups (dpg_team.h): S level-1 buckets; pt: the
+// buckets are the pieces of the histogram-free level 1.  Buckets whose
+// member share exceeds sub_cap records are skipped by the single-round
+// launch and done by a second, multi-round launch (k_part2_team kMulti), run
+// only when the host's level-1 totals (max_bucket) say one may exist.
 template <class R>
 int run_team_level2(dpg_ctx *ctx, hipStream_t s, const SrcAoS<R> &src, uint32_t S, uint32_t F2,
                     const int64_t *seg_start, const uint32_t *seg_cnt, R *out, Control *ctl,
-                    int64_t **base_out, uint32_t **tot_out, const PieceTab *pt = nullptr) {
+                    int64_t **base_out, uint32_t **tot_out, const PieceTab *pt,
+                    uint64_t max_bucket) {
     int st = DPG_OK;
     const uint32_t F = kTeamF;
     const size_t words = (size_t)8 * 3 * F + 8 * kTeamArriveStride + 32;
@@ -1303,16 +1324,41 @@ int run_team_level2(dpg_ctx *ctx, hipStream_t s, const SrcAoS<R> &src, uint32_t 
         k_set_bits<<<1, 1, 0, s>>>(&ctl->err, 8u);
         LAUNCH_CHECK();
     }
+    // records per member per round (test hook DPG_DEBUG_TEAM_SUB: a smaller,
+    // even cap, so that small inputs take the multi-round path)
+    uint32_t sub_cap = (uint32_t)kTeamSub;
+    if (const char *e = std::getenv("DPG_DEBUG_TEAM_SUB"))
+        sub_cap = std::min<uint32_t>(sub_cap, std::max<uint32_t>(2, (uint32_t)std::atoi(e)) & ~1u);
+    const uint32_t T = (uint32_t)ctx->n_cu / 8;
+    // a member's share: ceil(n / T) (+ 1, even, with up to 8 slots of piece padding)
+    const bool multi = (max_bucket + 8 + T - 1) / T + 2 > sub_cap;
     const void *k = pt ? (const void *)k_part2_team<R, true> : (const void *)k_part2_team<R, false>;
     (void)set_func_attr(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)team_lds<R>());
     stage(ctx, s, "partition2:team");
     if (pt)
         k_part2_team<R, true><<<(unsigned)ctx->n_cu, kScatThreads, team_lds<R>(), s>>>(
-            src, seg_start, seg_cnt, S, F2, out, base, tot, ts, *pt);
+            src, seg_start, seg_cnt, S, F2, out, base, tot, ts, *pt, sub_cap);
     else
         k_part2_team<R, false><<<(unsigned)ctx->n_cu, kScatThreads, team_lds<R>(), s>>>(
-            src, seg_start, seg_cnt, S, F2, out, base, tot, ts, PieceTab{});
+            src, seg_start, seg_cnt, S, F2, out, base, tot, ts, PieceTab{}, sub_cap);
     LAUNCH_CHECK();
+    if (multi) {
+        // the oversized buckets, in rounds; fresh team counters (the
+        // abort flag keeps its value: a timed-out first launch is redone
+        // anyway, err bit 8)
+        stage(ctx, s, "partition2:team_multi");
+        HIP_TRY(hipMemsetAsync(tw, 0, ((size_t)8 * 3 * F + 8 * kTeamArriveStride) * 4, s));
+        const void *km = pt ? (const void *)k_part2_team<R, true, true>
+                            : (const void *)k_part2_team<R, false, true>;
+        (void)set_func_attr(km, hipFuncAttributeMaxDynamicSharedMemorySize, (int)team_lds<R>());
+        if (pt)
+            k_part2_team<R, true, true><<<(unsigned)ctx->n_cu, kScatThreads, team_lds<R>(), s>>>(
+                src, seg_start, seg_cnt, S, F2, out, base, tot, ts, *pt, sub_cap);
+        else
+            k_part2_team<R, false, true><<<(unsigned)ctx->n_cu, kScatThreads, team_lds<R>(), s>>>(
+                src, seg_start, seg_cnt, S, F2, out, base, tot, ts, PieceTab{}, sub_cap);
+        LAUNCH_CHECK();
+    }
     *base_out = base;
     *tot_out = tot;
     return DPG_OK;
@@ -1387,7 +1433,7 @@ int pipeline(dpg_ctx *ctx, hipStream_t s, const int64_t *pid, const int64_t *pk,
                occ >= 1;
     }
     if (team && !ctx->pin_tot &&
-        hipHostMalloc((void **)&ctx->pin_tot, (size_t)4 * 4096, hipHostMallocDefault) != hipSuccess) {
+        hipHostMalloc((void **)&ctx->pin_tot, (size_t)4 * (kPinErr + 64), hipHostMallocDefault) != hipSuccess) {
         ctx->pin_tot = nullptr;
         team = false;
     }
@@ -1402,7 +1448,11 @@ int pipeline(dpg_ctx *ctx, hipStream_t s, const int64_t *pid, const int64_t *pk,
     // Round 4, without that prefetch, measured it a net loss (team 5.1 ->
     // 6.8 ms).
     constexpr int kIptPc = DPG_IPT_PC;
-    const int64_t subPc = (int64_t)kScatThreads * kIptPc;
+    // two 512-thread workgroups per CU for the 2048-digit piece level
+    // (DPG_PC_HALF=1)
+    const bool pc_half = F1 <= 2048 && env_int("DPG_PC_HALF", DPG_PC_HALF) != 0;
+    const int64_t subPc = (int64_t)(pc_half ? kScatThreads / 2 : kScatThreads) *
+                          (F1 > 2048 ? kIptL1W : kIptPc);
     uint32_t pcap = 0;
     bool pieces = false;
     if constexpr (sizeof(R) == 8) {
@@ -1418,32 +1468,44 @@ int pipeline(dpg_ctx *ctx, hipStream_t s, const int64_t *pid, const int64_t *pk,
     int64_t *bstart1 = nullptr;
     uint32_t *bcnt1 = nullptr;
     auto level1_std = [&](bool with_tot) -> int {
+        if constexpr (sizeof(R) == 8) {
+            if (F1 > 2048)  // a 12-bit level 1 (kMaxB1W)
+                return run_level<SrcSoAKey<R>, R, kIptL1W, 4096>(
+                    ctx, s, s1, 1u, nullptr, nullptr, &ctl->n_scalar, n, F1, pl.b1, recA,
+                    "partition1", &bstart1, &bcnt1, &ctl->ntiles[0], nullptr, l1_xcd, l1_subs,
+                    l1_grp, with_tot ? ctx->pin_tot : nullptr);
+        }
         return run_level<SrcSoAKey<R>, R, Ipt<R>::L1, 2048>(
             ctx, s, s1, 1u, nullptr, nullptr, &ctl->n_scalar, n, F1, pl.b1, recA, "partition1",
             &bstart1, &bcnt1, &ctl->ntiles[0], nullptr, l1_xcd, l1_subs, l1_grp,
             with_tot ? ctx->pin_tot : nullptr);
     };
     PieceTab ptab{};
+    uint64_t max_bucket = 0;  // the largest level-1 bucket (team launches)
     int r = DPG_OK;
     if constexpr (sizeof(R) == 8) {
         if (pieces) {
             SrcSoAKey<R, true> sp{pid, pk, p->public_mask, pl.P, pid_min, U, H, f,
                                   low_mask(pl.kbits - pl.b1 + pl.pkbits), pl.kbits - pl.b1,
                                   &ctl->err};
-            r = run_level1_pieces<R, kIptPc>(ctx, s, sp, n, F1, pl.b1, pcap, recA, ctl, &ptab,
-                                             ctx->pin_tot);
+            r = F1 > 2048 ? run_level1_pieces<R, kIptL1W, 4096>(ctx, s, sp, n, F1, pl.b1, pcap, recA,
+                                                               ctl, &ptab, ctx->pin_tot)
+                : pc_half ? run_level1_pieces<R, kIptPc, 2048, kScatThreads / 2>(
+                                ctx, s, sp, n, F1, pl.b1, pcap, recA, ctl, &ptab, ctx->pin_tot)
+                          : run_level1_pieces<R, kIptPc, 2048>(ctx, s, sp, n, F1, pl.b1, pcap, recA,
+                                                               ctl, &ptab, ctx->pin_tot);
             if (r) return r;
             HIP_TRY(hipEventSynchronize(ctx->tot_ev));
-            uint32_t mx = 0;
-            for (uint32_t d = 0; d < F1; ++d) mx = std::max(mx, ctx->pin_tot[d]);
-            const bool over = (ctx->pin_tot[4095] & 16u) != 0;
-            // a member's share is its 1/T of the padded bucket (<= 8 slots of
-            // padding) rounded up to even: within kTeamSub records
-            if (over || (uint64_t)mx + 8 > (uint64_t)team_T * (kTeamSub - 2)) {
-                std::fprintf(stderr, "[dpg] histogram-free level 1: %s; redone with the histogram path\n",
-                             over ? "a region overflowed" : "a bucket exceeds the team capacity");
+            for (uint32_t d = 0; d < F1; ++d) max_bucket = std::max<uint64_t>(max_bucket, ctx->pin_tot[d]);
+            const bool over = (ctx->pin_tot[kPinErr] & 16u) != 0;
+            // (a bucket over the team's single-round capacity takes the
+            // multi-round team launch, run_team_level2)
+            if (over) {
+                std::fprintf(stderr, "[dpg] histogram-free level 1: a region overflowed; redone "
+                                     "with the histogram path\n");
                 HIP_TRY(hipMemsetAsync(&ctl->err, 0, 4, s));
                 pieces = false;
+                max_bucket = 0;
             }
         }
     }
@@ -1452,9 +1514,7 @@ int pipeline(dpg_ctx *ctx, hipStream_t s, const int64_t *pid, const int64_t *pk,
         if (r) return r;
         if (team) {
             HIP_TRY(hipEventSynchronize(ctx->tot_ev));
-            uint32_t mx = 0;
-            for (uint32_t d = 0; d < F1; ++d) mx = std::max(mx, ctx->pin_tot[d]);
-            team = (uint64_t)mx <= (uint64_t)team_T * kTeamSub;
+            for (uint32_t d = 0; d < F1; ++d) max_bucket = std::max<uint64_t>(max_bucket, ctx->pin_tot[d]);
         }
     }
     bstart = bstart1;
@@ -1491,7 +1551,7 @@ int pipeline(dpg_ctx *ctx, hipStream_t s, const int64_t *pid, const int64_t *pk,
             if (team) {
                 SrcAoS<R> s2{recA, f, shift2, F2 - 1};
                 r = run_team_level2<R>(ctx, s, s2, F1, F2, bstart1, bcnt1, recB, ctl, &bstart, &bcnt,
-                                       pieces ? &ptab : nullptr);
+                                       pieces ? &ptab : nullptr, max_bucket);
             }
         }
         if (!team) {
@@ -1614,6 +1674,18 @@ int aggregate_impl(dpg_ctx *ctx, const int64_t *pid, const int64_t *pk, const do
     // one level up to 11 bits; beyond, the smaller half first (level 1 reads
     // 16 B per record, so its runs should be the longer ones)
     pl.b1 = bits_total <= kMaxB1 ? bits_total : bits_total / 2;
+    // level-1 buckets within the team level 2's single round (T members x
+    // kTeamSub records, 5 % slack): e.g. N = 1e9 with 2^20 privacy-id hash
+    // values (20 bits: 10 + 10 by halves) takes 11 + 9, whose ~490K-record
+    // buckets fit, instead of 1024 buckets of ~980K that all need the
+    // multi-round team launch (applies when level 2 keeps >= 6 bits)
+    if (bits_total > kMaxB1 && ctx->n_cu >= 8) {
+        const double cap = 0.95 * (double)(ctx->n_cu / 8) * (double)kTeamSub;
+        uint32_t need = 0;
+        while (need < kMaxB1 && (double)n / (double)(1u << need) > cap) ++need;
+        const uint32_t b1 = std::min<uint32_t>(std::max<uint32_t>(pl.b1, need), bits_total - 6);
+        if (b1 <= kMaxB1 && b1 > pl.b1) pl.b1 = b1;
+    }
     pl.b2 = bits_total - pl.b1;
     if (const char *e = std::getenv("DPG_DEBUG_B1")) {  // debug: level split experiments
         const uint32_t b1 = (uint32_t)std::atoi(e);
@@ -1624,6 +1696,17 @@ int aggregate_impl(dpg_ctx *ctx, const int64_t *pid, const int64_t *pk, const do
     }
     pl.plb = pl.kbits - bits_total;
     const uint32_t ib = std::max<uint32_t>(1, bits_for((uint64_t)n));
+    // 23-bit plans (N > 2^30): 12 + 11 bits instead of 11 + 12 when the
+    // records are then 8 bytes (not for the utility pre-aggregate's R16
+    // records), so that level 1 runs without a histogram pass and level 2
+    // by teams, as at smaller N
+    const char *b1w = std::getenv("DPG_B1W");  // "0": keep 11 + 12 (A/B)
+    if (!pa && bits_total == kMaxB1 + 12 && std::getenv("DPG_DEBUG_B1") == nullptr &&
+        !(b1w && std::atoi(b1w) == 0) &&
+        (pl.kbits - kMaxB1W) + pl.pkbits + ib <= 64) {
+        pl.b1 = kMaxB1W;
+        pl.b2 = bits_total - kMaxB1W;
+    }
     const bool r8 = (pl.kbits - pl.b1) + pl.pkbits + ib <= 64;
     // the utility pre-aggregate sums every record's value: R16 records carry
     // it (DPG_PA_GATHER=1: gather by index as the bounded paths do)

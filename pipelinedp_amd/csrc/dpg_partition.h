@@ -767,59 +767,77 @@ __device__ __forceinline__ uint32_t scatter_scan_update(uint32_t *cnt, uint32_t 
 // then calls scatter_rsv_finish; the atomic's round trip (and, being younger
 // in the vmcnt order, the drain of the previous write-out's stores) overlaps
 // the staging instead of stalling the scan.
+template <int DPT>
 struct PcRsv {
-    uint32_t c[2];  // the thread's two digit counts
-    uint32_t e0;    // local start of its first digit
-    unsigned long long old;
+    uint32_t c[DPT];  // the thread's digit counts
+    uint32_t e0;      // local start of its first digit
+    unsigned long long old[DPT / 2];
 };
+// NT threads, DPT (even) consecutive digits per thread: DPT / 2 64-bit
+// reservations per thread
+template <int NT, int DPT>
 __device__ __forceinline__ uint32_t scatter_scan_pc(uint32_t *cnt, uint32_t *dstart, uint32_t F,
-                                                    uint32_t *sh16, uint32_t *goff, PcRsv &r) {
-    const uint32_t d0 = 2 * threadIdx.x;
-    r.c[0] = d0 < F ? cnt[d0] : 0u;
-    r.c[1] = d0 + 1 < F ? cnt[d0 + 1] : 0u;
-    // unconditional (threads past F add 0 to the first pair): a result that
-    // is waited for on one path only is waited for again, with vmcnt(0),
-    // when its register is next overwritten -- after the prefetch loads
-    r.old = atomicAdd(reinterpret_cast<unsigned long long *>(&goff[d0 < F ? d0 : 0u]),
-                      (unsigned long long)r.c[0] | ((unsigned long long)r.c[1] << 32));
+                                                    uint32_t *sh16, uint32_t *goff, PcRsv<DPT> &r) {
+    const uint32_t d0 = DPT * threadIdx.x;
+    uint32_t x = 0;
+#pragma unroll
+    for (int u = 0; u < DPT; ++u) {
+        r.c[u] = d0 + u < F ? cnt[d0 + u] : 0u;
+        x += r.c[u];
+    }
+    // unconditional (threads past F add 0 to a pair of cursors d mod F: a
+    // result that is waited for on one path only is waited for again, with
+    // vmcnt(0), when its register is next overwritten -- after the prefetch
+    // loads).  Not one fixed dummy pair: with F < DPT NT its same-address
+    // atomics serialised in L2 (a 1024-digit level 1 ran 17x slower)
+#pragma unroll
+    for (int q = 0; q < DPT / 2; ++q)
+        r.old[q] = atomicAdd(reinterpret_cast<unsigned long long *>(&goff[(d0 + 2 * q) % F]),
+                             (unsigned long long)r.c[2 * q] | ((unsigned long long)r.c[2 * q + 1] << 32));
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     uint32_t wt;
-    uint32_t e = wave_excl_scan(r.c[0] + r.c[1], wt);
+    uint32_t e = wave_excl_scan(x, wt);
     if (lane == 63) sh16[w] = wt;
     __syncthreads();
     uint32_t total = 0;
 #pragma unroll
-    for (int k = 0; k < kScatThreads / 64; ++k) {
+    for (int k = 0; k < NT / 64; ++k) {
         const uint32_t y = sh16[k];
         if (k < w) e += y;
         total += y;
     }
     r.e0 = e;
-    if (d0 < F) {
-        dstart[d0] = e;
-        cnt[d0] = 0;
-    }
-    if (d0 + 1 < F) {
-        dstart[d0 + 1] = e + r.c[0];
-        cnt[d0 + 1] = 0;
+#pragma unroll
+    for (int u = 0; u < DPT; ++u) {
+        if (d0 + u < F) {
+            dstart[d0 + u] = e;
+            cnt[d0 + u] = 0;
+        }
+        e += r.c[u];
     }
     if (threadIdx.x == 0) dstart[F] = total;
     __syncthreads();
     return total;
 }
-// cur[d] of the thread's two digits from the reservation (lb: the regions'
+// cur[d] of the thread's digits from the reservations (lb: the regions'
 // bases); a run past the region's capacity goes to the dump area and raises
 // err bit 16.  The caller's next barrier publishes cur.
-__device__ __forceinline__ void scatter_rsv_finish(const PcRsv &r, uint32_t *cur, const uint32_t *lb,
-                                                   uint32_t F, uint32_t cap, uint32_t dump,
-                                                   uint32_t *err) {
-    const uint32_t d0 = 2 * threadIdx.x;
+template <int DPT>
+__device__ __forceinline__ void scatter_rsv_finish(const PcRsv<DPT> &r, uint32_t *cur,
+                                                   const uint32_t *lb, uint32_t F, uint32_t cap,
+                                                   uint32_t dump, uint32_t *err) {
+    const uint32_t d0 = DPT * threadIdx.x;
     // the returned cursors are consumed on every path (see scatter_scan_pc)
-    const uint32_t o[2] = {(uint32_t)r.old, (uint32_t)(r.old >> 32)};
+    uint32_t o[DPT];
+#pragma unroll
+    for (int q = 0; q < DPT / 2; ++q) {
+        o[2 * q] = (uint32_t)r.old[q];
+        o[2 * q + 1] = (uint32_t)(r.old[q] >> 32);
+    }
     uint32_t e = r.e0;
     bool over = false;
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < DPT; ++u) {
         const bool fits = o[u] + r.c[u] <= cap;
         const uint32_t v = fits ? (lb[d0 + u < F ? d0 + u : 0u] + o[u] + r.c[u]) : dump + e + r.c[u];
         if (d0 + u < F && r.c[u]) {
@@ -905,10 +923,10 @@ __device__ __forceinline__ T from_words(const Words<T> &x) {
 
 // LDS bytes of one k_scatter instantiation (one dummy staging slot past the
 // sub-tile for records that are dropped).
-template <class Src, class Rec, int IPT, int FMAX>
+template <class Src, class Rec, int IPT, int FMAX, int NT = kScatThreads>
 constexpr size_t scatter_lds_core() {
-    return (size_t)sizeof(Rec) * (kScatThreads * IPT + 1) +
-           (Src::kDigitFromRec ? 0 : a16((size_t)2 * (kScatThreads * IPT + 1))) +
+    return (size_t)sizeof(Rec) * (NT * IPT + 1) +
+           (Src::kDigitFromRec ? 0 : a16((size_t)2 * (NT * IPT + 1))) +
            (size_t)FMAX * 12 + 80;
 }
 // Grouped / piece modes keep the current segment's digit bases in LDS
@@ -925,14 +943,14 @@ constexpr size_t scatter_lds_core() {
 #ifndef DPG_PC_LATE_RSV
 #define DPG_PC_LATE_RSV 1
 #endif
-template <class Src, class Rec, int IPT, int FMAX>
+template <class Src, class Rec, int IPT, int FMAX, int NT = kScatThreads>
 constexpr bool scatter_lbase() {
-    return scatter_lds_core<Src, Rec, IPT, FMAX>() + (size_t)FMAX * 4 <= 160 * 1024;
+    return scatter_lds_core<Src, Rec, IPT, FMAX, NT>() + (size_t)FMAX * 4 <= 160 * 1024;
 }
-template <class Src, class Rec, int IPT, int FMAX>
+template <class Src, class Rec, int IPT, int FMAX, int NT = kScatThreads>
 constexpr size_t scatter_lds() {
-    return scatter_lds_core<Src, Rec, IPT, FMAX>() +
-           (scatter_lbase<Src, Rec, IPT, FMAX>() ? (size_t)FMAX * 4 : 0);
+    return scatter_lds_core<Src, Rec, IPT, FMAX, NT>() +
+           (scatter_lbase<Src, Rec, IPT, FMAX, NT>() ? (size_t)FMAX * 4 : 0);
 }
 
 // Phase clock of k_scatter (timing build only, -DDPG_PHASE_TIMING): wave 0
@@ -957,11 +975,21 @@ __device__ unsigned long long g_scat_cyc[8];
     } while (0)
 #endif
 
+// A pointer made provably uniform (scalar-load operands: dpg_team.h
+// sload_desc; a pointer the compiler keeps in vector registers is not one).
+template <class T>
+__device__ __forceinline__ const T *uniform_ptr(const T *p) {
+    const uint64_t v = (uint64_t)(uintptr_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return reinterpret_cast<const T *>((uintptr_t)(((uint64_t)hi << 32) | lo));
+}
+
 // kAgg: wave-aggregated ranking (few digits) instead of one LDS atomic per
 // record; a template parameter so that each kernel holds one ranking path
 // (both paths in one kernel cost the hot one its registers)
-template <class Src, class Rec, int IPT, int FMAX, bool kAgg>
-__global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const TileDesc *tiles,
+template <class Src, class Rec, int IPT, int FMAX, bool kAgg, int NT = kScatThreads>
+__global__ __launch_bounds__(NT, 4) void k_scatter(Src src_in, const TileDesc *tiles,
                                                           const uint32_t *ntiles, uint32_t F,
                                                           uint32_t bits, const uint32_t *off,
                                                           const int64_t *base, Rec *out,
@@ -972,7 +1000,7 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
                                                           uint32_t C = 1, uint32_t *goff = nullptr,
                                                           uint32_t pcap = 0, uint32_t pdump = 0,
                                                           uint32_t *perr = nullptr) {
-    constexpr int SUB = kScatThreads * IPT;
+    constexpr int SUB = NT * IPT;
     // piece mode (histogram-free level 1): one-sub-tile tiles on a static
     // schedule; workgroup b appends its runs of digit d to region (b % 8, d)
     // -- base[(b % 8) F + d], cursor goff[(b % 8) F + d], pcap records -- so
@@ -989,24 +1017,26 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
     uint32_t *dstart = cnt + FMAX;
     uint32_t *cur = dstart + FMAX + 1;  // output positions (n < 2^32 per device)
     uint32_t *sh16 = cur + FMAX;
-    constexpr bool kLB = DPG_SCAT_LBASE && scatter_lbase<Src, Rec, IPT, FMAX>();
-    uint32_t *lbase = reinterpret_cast<uint32_t *>(smem + scatter_lds_core<Src, Rec, IPT, FMAX>());
+    constexpr bool kLB = DPG_SCAT_LBASE && scatter_lbase<Src, Rec, IPT, FMAX, NT>();
+    uint32_t *lbase = reinterpret_cast<uint32_t *>(smem + scatter_lds_core<Src, Rec, IPT, FMAX, NT>());
     uint32_t lseg = 0xFFFFFFFFu;  // segment whose bases lbase holds
 
     // persistent over the tiles.  XCD-local mode (xq.q): workgroup b serves
     // the queue of XCD b % 8 (round-robin placement), taking the next tile id
     // by one atomic per tile, so an XCD's workgroups work on the same
     // segments at the same time and their runs meet in that XCD's L2
-    const uint32_t nt = *ntiles;
+    const uint32_t nt = __builtin_amdgcn_readfirstlane(*ntiles);
     const int tid = threadIdx.x;
     // sub-tile position of this thread's element j
     auto elem = [tid](int j) -> uint32_t {
-        return kP ? (uint32_t)((j >> 1) * 2 * kScatThreads + 2 * tid + (j & 1))
-                  : (uint32_t)(j * kScatThreads + tid);
+        return kP ? (uint32_t)((j >> 1) * 2 * NT + 2 * tid + (j & 1))
+                  : (uint32_t)(j * NT + tid);
     };
     __shared__ uint32_t sh_next;
     const uint32_t xq_id = blockIdx.x & 7u;
-    const uint32_t xq_len = xq.q ? xq.n[xq_id] : 0u;
+    // (uniform: the loop over the tiles holds barriers, so its exits must
+    // be visibly wave-uniform -- tools/check_barrier_loops.py)
+    const uint32_t xq_len = xq.q ? __builtin_amdgcn_readfirstlane(xq.n[xq_id]) : 0u;
     constexpr uint32_t kNone = 0xFFFFFFFFu;
     Src src = src_in;  // per-thread copy (sources may cache lookup state)
     // software pipeline: the raw loads of the next sub-tile -- of this tile,
@@ -1030,7 +1060,7 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
             if (lim >= 2) {
 #pragma unroll
                 for (int m = 0; m < IPT / 2; ++m) {
-                    const uint32_t o = m * 2 * kScatThreads + 2 * tid;
+                    const uint32_t o = m * 2 * NT + 2 * tid;
                     const uint32_t a = min(o, lim - 2);
                     typename Src::Raw x0, x1;
                     src.fetch2(b0 + a, x0, x1);
@@ -1072,7 +1102,7 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
     // every tile transition.
     constexpr bool kPcLB = kPc && kLB && DPG_PC_NORESET;
     if constexpr (kPcLB) {
-        for (uint32_t d = tid; d < F; d += kScatThreads) {
+        for (uint32_t d = tid; d < F; d += NT) {
             lbase[d] = (uint32_t)base[(size_t)(blockIdx.x & 7u) * F + d];
             cnt[d] = 0;
         }
@@ -1098,15 +1128,15 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
     if (kLB && goff) {
         // a thread reads back only the lbase entries it wrote itself
         if (bsel != lseg) {
-            for (uint32_t d = tid; d < F; d += kScatThreads) lbase[d] = (uint32_t)base[(size_t)bsel * F + d];
+            for (uint32_t d = tid; d < F; d += NT) lbase[d] = (uint32_t)base[(size_t)bsel * F + d];
             lseg = bsel;
         }
-        for (uint32_t d = tid; d < F; d += kScatThreads) {
+        for (uint32_t d = tid; d < F; d += NT) {
             cur[d] = lbase[d];
             cnt[d] = 0;
         }
     } else {
-        for (uint32_t d = tid; d < F; d += kScatThreads) {
+        for (uint32_t d = tid; d < F; d += NT) {
             cur[d] = (uint32_t)(base[(size_t)bsel * F + d] +
                                 (goff ? 0u : off[(size_t)t * F + d] + (cb ? cb[d] : 0u)));
             cnt[d] = 0;
@@ -1154,13 +1184,14 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
         if (xq.q && tid == 0 && sb == td.begin) sh_next = nq;
         __syncthreads();
         DPG_SCAT_MARK(0);
-        constexpr bool kLate = kPcLB && FMAX == 2 * kScatThreads && DPG_PC_LATE_RSV;
-        PcRsv rsv;
+        constexpr int kDPT = FMAX / NT;
+        constexpr bool kLate = kPcLB && (kDPT == 2 || kDPT == 4) && FMAX == kDPT * NT && DPG_PC_LATE_RSV;
+        PcRsv<(kDPT >= 2 ? kDPT : 2)> rsv;
         uint32_t total;
         if constexpr (kLate)
-            total = scatter_scan_pc(cnt, dstart, F, sh16, gof, rsv);
+            total = scatter_scan_pc<NT, kDPT>(cnt, dstart, F, sh16, gof, rsv);
         else
-            total = scatter_scan_update<kScatThreads, FMAX / kScatThreads, kPc>(
+            total = scatter_scan_update<NT, FMAX / NT, kPc>(
                 cnt, dstart, cur, F, sh16, gof, pcap, pdump, perr, kPcLB ? lbase : nullptr);
         DPG_SCAT_MARK(1);
         {
@@ -1222,7 +1253,7 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
             uint32_t dd[WB], kc[WB];
 #pragma unroll
             for (int u = 0; u < WB; ++u) {
-                kc[u] = min(k0 + u * kScatThreads + tid, total - 1);
+                kc[u] = min(k0 + u * NT + tid, total - 1);
                 x[u] = stage[kc[u]];
                 if constexpr (kSD) dd[u] = sdig[kc[u]];
             }
@@ -1255,11 +1286,11 @@ __global__ __launch_bounds__(kScatThreads) void k_scatter(Src src_in, const Tile
         if constexpr (kPc) {
 #pragma unroll
             for (int b = 0; b < kWbIter; ++b) {
-                if ((uint32_t)b * WB * kScatThreads >= total) break;
-                write_batch((uint32_t)b * WB * kScatThreads);
+                if ((uint32_t)b * WB * NT >= total) break;
+                write_batch((uint32_t)b * WB * NT);
             }
         } else {
-            for (uint32_t k0 = 0; k0 < total; k0 += WB * kScatThreads) write_batch(k0);
+            for (uint32_t k0 = 0; k0 < total; k0 += WB * NT) write_batch(k0);
         }
         // the next sub-tile's first barrier (after its ranking) orders this
         // write-out's LDS reads before the next scan and staging

@@ -152,6 +152,7 @@ typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
 // 128 bytes at a uniform, 64-byte aligned address into scalar registers
 // (loads only: nothing is written through the scalar cache)
 __device__ __forceinline__ void sload_desc(const PieceDesc *p, u32x16 &a, u32x16 &b) {
+    p = uniform_ptr(p);
     asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx16 %1, %2, 0x40\n\ts_waitcnt lgkmcnt(0)"
                  : "=s"(a), "=s"(b)
                  : "s"(p)
@@ -166,13 +167,24 @@ __device__ __forceinline__ void sload_desc(const PieceDesc *p, u32x16 &a, u32x16
 // resident.  kPc: the buckets are PieceTab pieces (seg_start / seg_cnt
 // unused), read with one 8-byte load per record (a piece may start at an odd
 // record), written compactly from ostart[s].
-template <class R, bool kPc = false>
+//
+// kMulti: a member's share may exceed the kTeamSub records its registers and
+// LDS stage hold (heavy privacy ids or N past 2^30 make level-1 buckets
+// larger than T kTeamSub).  A bucket whose share exceeds sub_cap (<= kTeamSub,
+// even) is done in J = ceil(share / sub_cap) rounds: pass A loads the rounds
+// one after another and only counts digits, the member reserves its runs of
+// all rounds at once, the team barrier publishes the totals, and pass B
+// reloads each round, ranks, stages and writes it at the member's advancing
+// run cursors -- one more read of the bucket, the same output layout.
+// Buckets that fit take the single-round path unchanged.
+template <class R, bool kPc = false, bool kMulti = false>
 __global__ __launch_bounds__(kScatThreads) void k_part2_team(SrcAoS<R> src,
                                                              const int64_t *seg_start,
                                                              const uint32_t *seg_cnt, uint32_t S,
                                                              uint32_t F2, R *out, int64_t *base_out,
                                                              uint32_t *tot_out, TeamSync ts,
-                                                             PieceTab pt = PieceTab{}) {
+                                                             PieceTab pt = PieceTab{},
+                                                             uint32_t sub_cap = kTeamSub) {
     constexpr int IPT = kTeamIPT;
     constexpr int SUB = kTeamSub;
     constexpr uint32_t F = kTeamF;
@@ -207,7 +219,7 @@ __global__ __launch_bounds__(kScatThreads) void k_part2_team(SrcAoS<R> src,
                        (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)st0));
         const uint32_t q = kPc ? (((n + T - 1) / T + 1) & ~1u) : (n + T - 1) / T;
         b0 = min(n, m * q);
-        lim = min(n, b0 + q) - b0;  // <= SUB (host check)
+        lim = min(n, b0 + q) - b0;  // <= sub_cap <= SUB, or the bucket is the kMulti launch's
     };
     R rec[IPT];
     uint32_t vmask = ~0u;  // piece mode: bit j = element j is a record (not padding)
@@ -320,10 +332,17 @@ __global__ __launch_bounds__(kScatThreads) void k_part2_team(SrcAoS<R> src,
     // barrier and write-out (the local staging moves before the barrier,
     // which frees the record registers); pf_s = the bucket those registers
     // hold
-    constexpr bool kPF = DPG_TEAM_PF && (!kPc || DPG_TEAM_PF_PC);
+    constexpr bool kPF = DPG_TEAM_PF && (!kPc || DPG_TEAM_PF_PC) && !kMulti;
+    // a member's share of n records (team-uniform): over sub_cap, the bucket
+    // is left to the kMulti launch
+    auto share_q = [&](uint32_t n) -> uint32_t {
+        return kPc ? (((n + T - 1) / T + 1) & ~1u) : (n + T - 1) / T;
+    };
     auto next_nonempty = [&](uint32_t s) -> uint32_t {
-        for (; s < S; s += 8)
-            if (__builtin_amdgcn_readfirstlane(kPc ? pt.ptot[s] : seg_cnt[s]) != 0) break;
+        for (; s < S; s += 8) {
+            const uint32_t n = __builtin_amdgcn_readfirstlane(kPc ? pt.ptot[s] : seg_cnt[s]);
+            if (n != 0 && share_q(n) <= sub_cap) break;
+        }
         return s;
     };
     // the loads of one share (piece mode: its 8-piece descriptors first);
@@ -342,7 +361,7 @@ __global__ __launch_bounds__(kScatThreads) void k_part2_team(SrcAoS<R> src,
                 // so the barrier's first poll is waited for by count
                 u32x16 da, db;
                 sload_desc(pt.desc + min(s, S - 1), da, db);
-                pf_n = da[0];
+                pf_n = __builtin_amdgcn_readfirstlane(da[0]);
                 pf_st = (int64_t)(((uint64_t)da[3] << 32) | da[2]);
                 const uint32_t q = ((pf_n + T - 1) / T + 1) & ~1u;
                 pf_b0 = min(pf_n, m * q);
@@ -364,6 +383,30 @@ __global__ __launch_bounds__(kScatThreads) void k_part2_team(SrcAoS<R> src,
         pf_s = next_nonempty(team);
         if (use_desc || pf_s < S) load_share(pf_s);
     }
+    // the staged records [0, nv) to their runs: out[st + cur[d] + (k -
+    // dstart[d])] for staged position k of digit d
+    auto write_out = [&](int64_t st, uint32_t nv) {
+        constexpr int WB = DPG_TEAM_WB;
+        for (uint32_t k0 = 0; k0 < nv; k0 += WB * kScatThreads) {
+            W x[WB];
+            uint32_t dd[WB], kc[WB];
+#pragma unroll
+            for (int u = 0; u < WB; ++u) {
+                kc[u] = min(k0 + u * kScatThreads + tid, nv - 1);
+                x[u] = stage[kc[u]];
+                dd[u] = src.digit(from_words<R>(x[u]));
+            }
+            uint32_t c1[WB], c2[WB];
+#pragma unroll
+            for (int u = 0; u < WB; ++u) {
+                c1[u] = cur[dd[u]];
+                c2[u] = dstart[dd[u]];
+            }
+#pragma unroll
+            for (int u = 0; u < WB; ++u)
+                *reinterpret_cast<W *>(&out[st + c1[u] + (kc[u] - c2[u])]) = x[u];
+        }
+    };
     for (uint32_t s = team; s < S; s += 8) {
         int64_t st;
         uint32_t n, b0, lim;
@@ -379,14 +422,155 @@ __global__ __launch_bounds__(kScatThreads) void k_part2_team(SrcAoS<R> src,
         } else {
             share(s, st, n, b0, lim);
         }
-        if (n == 0) {
-            if (m == 0)
-                for (uint32_t d = tid; d < F2; d += kScatThreads) {
-                    base_out[(size_t)s * F2 + d] = st;
-                    tot_out[(size_t)s * F2 + d] = 0;
-                }
-            continue;  // uniform over the team: no barrier
+        if constexpr (kMulti) {
+            if (n == 0 || share_q(n) <= sub_cap) continue;  // the single-round launch's
+        } else {
+            if (n == 0) {
+                if (m == 0)
+                    for (uint32_t d = tid; d < F2; d += kScatThreads) {
+                        base_out[(size_t)s * F2 + d] = st;
+                        tot_out[(size_t)s * F2 + d] = 0;
+                    }
+                continue;  // uniform over the team: no barrier
+            }
+            if (share_q(n) > sub_cap) continue;  // left to the kMulti launch (uniform)
         }
+        // ---- the bucket's digit starts from the team totals (after the
+        // team barrier): cur += digit start; member 0 writes the fine
+        // buckets' starts and counts and zeroes the totals of the bucket
+        // after next
+        auto team_starts = [&](const uint32_t *tt) {
+            const uint32_t d0 = DPT * tid;
+            uint32_t c[DPT], x = 0;
+#pragma unroll
+            for (int u = 0; u < DPT; ++u) {
+                c[u] = ld_agent(&tt[d0 + u]);
+                x += c[u];
+            }
+            uint32_t wt;
+            uint32_t e = wave_excl_scan(x, wt);
+            if (lane == 63) sh16[wv] = wt;
+            __syncthreads();
+#pragma unroll
+            for (int w = 0; w < kScatThreads / 64; ++w)
+                if (w < wv) e += sh16[w];
+            uint32_t *tz = ts.tot + ((size_t)team * 3 + (k + 1) % 3) * F;  // the bucket after next
+#pragma unroll
+            for (int u = 0; u < DPT; ++u) {
+                cur[d0 + u] += e;
+                if (m == 0) {
+                    if (d0 + u < F2) {
+                        base_out[(size_t)s * F2 + d0 + u] = st + e;
+                        tot_out[(size_t)s * F2 + d0 + u] = c[u];
+                    }
+                    __hip_atomic_store(&tz[d0 + u], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                e += c[u];
+            }
+        };
+        if constexpr (kMulti) {
+            const uint32_t q = share_q(n);
+            {
+                uint32_t *tt = ts.tot + ((size_t)team * 3 + k % 3) * F;
+                const uint32_t J = (q + sub_cap - 1) / sub_cap;
+                auto load_part = [&](uint32_t j, uint32_t &lj) {
+                    const uint32_t bj = b0 + j * sub_cap;
+                    lj = lim > j * sub_cap ? min(sub_cap, lim - j * sub_cap) : 0u;
+                    if constexpr (kPc) {
+                        if constexpr (use_desc) {
+                            u32x16 da, db;
+                            sload_desc(pt.desc + s, da, db);
+                            load_pieces_desc(da, db, bj, max(lj, 2u));
+                        } else {
+                            vmask = 0;
+                            if (lj > 0) load_pieces(s, bj, lj);
+                        }
+                    } else {
+                        load(st + bj, lj);
+                    }
+                };
+                auto ok_elem = [&](int jj, uint32_t lj) {
+                    bool ok = elem(jj) < lj;
+                    if constexpr (kPc) ok = ok && ((vmask >> jj) & 1u);
+                    return ok;
+                };
+                // ---- pass A: the member's digit counts over all its rounds
+                for (uint32_t j = 0; j < J; ++j) {
+                    uint32_t lj;
+                    load_part(j, lj);
+#pragma unroll
+                    for (int jj = 0; jj < IPT; ++jj) {
+                        const bool ok = ok_elem(jj, lj);
+                        atomicAdd(&cnt[ok ? src.digit(rec[jj]) : 0u], ok ? 1u : 0u);
+                    }
+                }
+                __syncthreads();
+                {
+                    const uint32_t d0 = DPT * tid;
+#pragma unroll
+                    for (int u = 0; u < DPT; ++u) {
+                        cur[d0 + u] = atomicAdd(&tt[d0 + u], cnt[d0 + u]);
+                        cnt[d0 + u] = 0;
+                    }
+                }
+                ++k;
+                if (!team_barrier(ts, team, T * k, &sh_ok)) return;
+                team_starts(tt);
+                // ---- pass B: each round ranked, staged and written at the
+                // member's run cursors, which then advance by its counts
+                for (uint32_t j = 0; j < J; ++j) {
+                    __syncthreads();  // the previous round's write-out / cursor updates
+                    uint32_t lj;
+                    load_part(j, lj);
+                    uint32_t drm[IPT];
+#pragma unroll
+                    for (int jj = 0; jj < IPT; ++jj) {
+                        const bool ok = ok_elem(jj, lj);
+                        const uint32_t dg = ok ? src.digit(rec[jj]) : 0u;
+                        const uint32_t rk = atomicAdd(&cnt[dg], ok ? 1u : 0u);
+                        drm[jj] = ok ? (dg | (rk << 12)) : ~0u;
+                    }
+                    __syncthreads();
+                    const uint32_t d0 = DPT * tid;
+                    uint32_t c[DPT], x = 0;
+#pragma unroll
+                    for (int u = 0; u < DPT; ++u) {
+                        c[u] = cnt[d0 + u];
+                        x += c[u];
+                    }
+                    uint32_t wt;
+                    uint32_t e = wave_excl_scan(x, wt);
+                    if (lane == 63) sh16[wv] = wt;
+                    __syncthreads();
+                    uint32_t nvj = 0;
+#pragma unroll
+                    for (int w = 0; w < kScatThreads / 64; ++w) {
+                        if (w < wv) e += sh16[w];
+                        nvj += sh16[w];
+                    }
+#pragma unroll
+                    for (int u = 0; u < DPT; ++u) {
+                        dstart[d0 + u] = e;
+                        cnt[d0 + u] = 0;
+                        e += c[u];
+                    }
+                    __syncthreads();
+#pragma unroll
+                    for (int jj = 0; jj < IPT; ++jj) {
+                        const uint32_t pos = drm[jj] != ~0u ? dstart[drm[jj] & 0xFFFu] + (drm[jj] >> 12)
+                                                            : (uint32_t)SUB;
+                        stage[pos] = to_words(rec[jj]);
+                    }
+                    __syncthreads();
+                    write_out(st, nvj);
+                    __syncthreads();
+#pragma unroll
+                    for (int u = 0; u < DPT; ++u) cur[d0 + u] += c[u];
+                }
+                __syncthreads();
+                continue;
+            }
+        } else {
         uint32_t *tt = ts.tot + ((size_t)team * 3 + k % 3) * F;
         // ---- load + rank
         if constexpr (!kPF) load_share(s);
@@ -463,7 +647,9 @@ __global__ __launch_bounds__(kScatThreads) void k_part2_team(SrcAoS<R> src,
             }
         };
         if (!team_barrier(ts, team, T * k, &sh_ok, prefetch)) return;
-        // ---- the bucket's digit starts from the team totals
+        // ---- the bucket's digit starts from the team totals (the
+        // team_starts code, inline: as a lambda call it cost the single-round
+        // path 6 spilled VGPRs)
         {
             const uint32_t d0 = DPT * tid;
             uint32_t c[DPT], x = 0;
@@ -504,27 +690,30 @@ __global__ __launch_bounds__(kScatThreads) void k_part2_team(SrcAoS<R> src,
         __syncthreads();
         // (loading the next bucket's share during the write-out measured
         // slower: 5.2 -> 5.65 ms at config 2, 128 VGPRs with spills)
-        constexpr int WB = DPG_TEAM_WB;
-        for (uint32_t k0 = 0; k0 < nv; k0 += WB * kScatThreads) {
-            W x[WB];
-            uint32_t dd[WB], kc[WB];
+        {
+            constexpr int WB = DPG_TEAM_WB;
+            for (uint32_t k0 = 0; k0 < nv; k0 += WB * kScatThreads) {
+                W x[WB];
+                uint32_t dd[WB], kc[WB];
 #pragma unroll
-            for (int u = 0; u < WB; ++u) {
-                kc[u] = min(k0 + u * kScatThreads + tid, nv - 1);
-                x[u] = stage[kc[u]];
-                dd[u] = src.digit(from_words<R>(x[u]));
+                for (int u = 0; u < WB; ++u) {
+                    kc[u] = min(k0 + u * kScatThreads + tid, nv - 1);
+                    x[u] = stage[kc[u]];
+                    dd[u] = src.digit(from_words<R>(x[u]));
+                }
+                uint32_t c1[WB], c2[WB];
+#pragma unroll
+                for (int u = 0; u < WB; ++u) {
+                    c1[u] = cur[dd[u]];
+                    c2[u] = dstart[dd[u]];
+                }
+#pragma unroll
+                for (int u = 0; u < WB; ++u)
+                    *reinterpret_cast<W *>(&out[st + c1[u] + (kc[u] - c2[u])]) = x[u];
             }
-            uint32_t c1[WB], c2[WB];
-#pragma unroll
-            for (int u = 0; u < WB; ++u) {
-                c1[u] = cur[dd[u]];
-                c2[u] = dstart[dd[u]];
-            }
-#pragma unroll
-            for (int u = 0; u < WB; ++u)
-                *reinterpret_cast<W *>(&out[st + c1[u] + (kc[u] - c2[u])]) = x[u];
         }
         __syncthreads();  // dstart / cur / stage are rewritten by the next bucket
+        }  // !kMulti
     }
 }
 
