@@ -8,6 +8,8 @@
 #   4. bench lines: configs[1] (CPU baseline on), configs[3] private / public (CPU
 #      baseline on), configs[4], the (N = 1e9, U = 1e6) and (N = 2e9, U = 2e7) inputs;
 #   5. the config-5 host split.
+# SKIP_TESTS / SKIP_PMC (steps 2-3) / SKIP_BENCH (steps 4-5) split it over calls; a
+# bench-only call needs the profiles/hbm_traffic*.json of the PMC call copied back.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 export TMPDIR=/tmp
@@ -20,6 +22,7 @@ tail -1 $O/pytest_gpu.log
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo smoke failed; tail -20 $O/smoke.log; exit 1; }
 tail -1 $O/smoke.log
 fi
+if [ -z "$SKIP_PMC" ]; then
 cd /tmp
 B1="python3 $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline"
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- $B1 > /dev/null 2> $O/pmc_fetch.err || { echo fetch failed; tail -20 $O/pmc_fetch.err; exit 1; }
@@ -37,6 +40,8 @@ cd /tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/kt_bench.json 2> $O/kt.err || { echo kt failed; tail -20 $O/kt.err; exit 1; }
 cd $R
 python3 tools/kstats.py $(find $O/kt -name "*kernel_stats.csv" | head -1) 10
+fi
+[ -n "$SKIP_BENCH" ] && { echo done; exit 0; }
 summ() { python3 -c "import json,sys; d=json.load(open('$1')); print('$2', round(d['ms_per_step'],2), 'frac', round(d['roofline']['frac'],4), 'traffic', d['roofline'].get('traffic'), 'cpu', (d.get('cpu_baseline') or {}).get('value'))"; }
 timeout -k 10 600 python bench.py > $O/bench_c2.json 2> $O/bench_c2.err || { echo bench failed; tail -20 $O/bench_c2.err; exit 1; }
 summ $O/bench_c2.json c2
