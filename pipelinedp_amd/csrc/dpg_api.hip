@@ -807,7 +807,7 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
             b = 1;
         return b;
     };
-    const void *narrow = nullptr, *mid = nullptr, *wide = nullptr;
+    const void *narrow = nullptr, *mid = nullptr, *wide = nullptr, *medium = nullptr;
     size_t mid_lds = wave_lds, wide_lds = wave_lds;
     constexpr bool kMid = kHasMid<R>;
     if constexpr (!ItemTraits<Item>::preagg) {
@@ -815,6 +815,7 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
             narrow = (const void *)k_bound_sorted<Item, R, 0, false>;
             if constexpr (kMid) mid = (const void *)k_bound_sorted<Item, R, 1, false>;
             wide = (const void *)k_bound_sorted<Item, R, 2, false>;
+            medium = (const void *)k_bound_sorted<Item, R, 3, false>;
             wave_lds = SortLayout<Item, R, false, kTierCand<R, 0>>::TOTAL;
             mid_lds = SortLayout<Item, R, false, kTierCand<R, 1>>::TOTAL;
             wide_lds = SortLayout<Item, R, false, kTierCand<R, 2>>::TOTAL;
@@ -824,6 +825,7 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
                 narrow = (const void *)k_bound_sorted<Item, R, 0, true>;
                 if constexpr (kMid) mid = (const void *)k_bound_sorted<Item, R, 1, true>;
                 wide = (const void *)k_bound_sorted<Item, R, 2, true>;
+                medium = (const void *)k_bound_sorted<Item, R, 3, true>;
                 wave_lds = SortLayout<Item, R, true, kTierCand<R, 0>>::TOTAL;
                 mid_lds = SortLayout<Item, R, true, kTierCand<R, 1>>::TOTAL;
                 wide_lds = SortLayout<Item, R, true, kTierCand<R, 2>>::TOTAL;
@@ -833,9 +835,20 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     const int per_cu = use_sort ? waves_per_cu(narrow, wave_lds, 4 * kNarrowWPS<R>)
                                 : waves_per_cu((const void *)wave_kern, wave_lds);
     const uint32_t Gw = (uint32_t)(ctx->n_cu * per_cu);
-    const uint32_t Gm = hctl.n_mchunks ? (uint32_t)std::min<uint32_t>(
-                                             ctx->n_cu * CL::PER_CU, hctl.n_mchunks)
-                                       : 0u;
+    // medium chunks: streamed by single waves of the sort kernel (tier 3,
+    // the narrow pass's working set), the chunks it defers by the hash-table
+    // kernel; DPG_MEDIUM_STREAM=0 (or DPG_MW_MEDIUM): the workgroup kernels
+    // alone.  Pid slots need <= 7 hash bits below a bucket.
+    const char *ms_env = std::getenv("DPG_MEDIUM_STREAM");
+    const bool stream_med = medium != nullptr && hctl.n_mchunks > 0 && pl.plb <= 7 &&
+                            !(ms_env && std::atoi(ms_env) == 0) &&
+                            std::getenv("DPG_MW_MEDIUM") == nullptr;
+    const uint32_t Gm =
+        !hctl.n_mchunks ? 0u
+        : stream_med    ? (uint32_t)std::min<uint32_t>(
+                           ctx->n_cu * waves_per_cu(medium, wave_lds, 4 * kNarrowWPS<R>),
+                           hctl.n_mchunks)
+                        : (uint32_t)std::min<uint32_t>(ctx->n_cu * CL::PER_CU, hctl.n_mchunks);
     const uint32_t G = Gw + Gm;
     // heavy buckets handed back are counted twice (candidates + bucket)
     const int64_t items_cap = std::max<int64_t>(n + (heavy ? (int64_t)n_global * kWCap : 0), 1);
@@ -930,11 +943,43 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     if (prog) watchdog_wait(s, prog, Gw, "k_bound_waves");
     stage(ctx, s, "bound.medium");
     bool medium_done = false;
+    uint8_t *mdefer = nullptr;
     if constexpr (!ItemTraits<Item>::preagg) {
+        if (stream_med) {
+            WS(mdef, uint8_t, "bound.mdefer", hctl.n_mchunks);
+            mdefer = mdef;
+            // tier 3 shares the narrow pass's working set (kTierCand)
+            (void)set_func_attr(medium, hipFuncAttributeMaxDynamicSharedMemorySize, (int)wave_lds);
+            BoundParams bpm = bpl;
+            if (timing) bpm.phase_cyc = bpl.phase_cyc + 16;
+            auto launch_s = [&](auto wpk_tag) {
+                constexpr bool W = decltype(wpk_tag)::value;
+                k_bound_sorted<Item, R, 3, W><<<Gm, 64, wave_lds, s>>>(
+                    recs, refined, recs, mchunk_list, &ctl->n_mchunks, bpm, items, wg_off + Gw,
+                    wg_cnt + Gw, mdefer, Gm);
+            };
+            if (!wpk) {
+                launch_s(std::false_type{});
+            } else if constexpr (sizeof(R) == 12) {
+                launch_s(std::true_type{});
+            }
+            LAUNCH_CHECK();
+            stage(ctx, s, "bound.medium_deferred");
+            BoundParams bpd = bpl;
+            bpd.phase_cyc = nullptr;
+            (void)set_func_attr((const void *)k_bound_chunks_deferred<KeyT, Item, R>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)CL::TOTAL);
+            k_bound_chunks_deferred<KeyT, Item, R>
+                <<<std::min<uint32_t>(Gm, ctx->n_cu * CL::PER_CU), kBT, CL::TOTAL, s>>>(
+                    recs, refined, mchunk_list, &ctl->n_mchunks, bpd, items, wg_off + Gw,
+                    wg_cnt + Gw, mdefer, Gm);
+            LAUNCH_CHECK();
+            medium_done = true;
+        }
         // the 4-wave medium kernel measured slower than the hash-table one
         // (config 4 medium 9.8 vs 7.6 ms: a 1024-element sort for ~300
         // candidates): opt-in
-        if (Gm && use_mw && std::getenv("DPG_MW_MEDIUM") != nullptr) {
+        if (Gm && !medium_done && use_mw && std::getenv("DPG_MW_MEDIUM") != nullptr) {
             auto launch_m = [&](auto wpk_tag) {
                 constexpr bool W = decltype(wpk_tag)::value;
                 using LM = SortLayoutMW<Item, R, W, 4>;
@@ -988,7 +1033,9 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
             unsigned long long tot = 0;
             const bool sortnames =
                 part == 0 ? use_sort
-                          : use_mw && (part == 2 || std::getenv("DPG_MW_MEDIUM") != nullptr);
+                : part == 1 && stream_med
+                    ? true
+                    : use_mw && (part == 2 || std::getenv("DPG_MW_MEDIUM") != nullptr);
             const int np = sortnames ? 6 : part ? 9 : 12;
             for (int i = 0; i < np; ++i) tot += hp[i];
             std::fprintf(stderr, "[dpg phase] %s chunks=%u over=%u over2=%u per-WG Mcycles:",
@@ -999,6 +1046,14 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
                 std::fprintf(stderr, " %s=%.3f(%.0f%%)", nm[i], hp[i] / 1e6 / gg,
                              100.0 * hp[i] / (tot ? tot : 1));
             std::fprintf(stderr, "\n");
+        }
+        if (mdefer) {
+            std::vector<uint8_t> hd(hctl.n_mchunks);
+            HIP_TRY(hipMemcpy(hd.data(), mdefer, hd.size(), hipMemcpyDeviceToHost));
+            size_t nd = 0;
+            for (uint8_t x : hd) nd += x;
+            std::fprintf(stderr, "[dpg phase] medium chunks streamed=%u deferred=%zu\n",
+                         hctl.n_mchunks, nd);
         }
     }
     // ---- single buckets beyond the chunk capacity: global-memory working sets

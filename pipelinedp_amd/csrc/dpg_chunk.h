@@ -638,6 +638,52 @@ __global__ __launch_bounds__(kBT) void k_bound_chunks(const R *recs, const R *re
     timer_flush(bp, clk);
 }
 
+// The medium chunks the streamed sort pass (dpg_sortb.h, tier 3) deferred
+// (defer[w] set: more candidates than its working set holds): workgroup g2
+// takes the streamed pass's workgroups g = g2, g2 + gridDim.x, ... (of G1)
+// and bounds their flagged chunks, appending behind wg_cnt[g].
+template <class KeyT, class Item, class R>
+__global__ __launch_bounds__(kBT) void k_bound_chunks_deferred(
+    const R *recs, const R *refined, const uint4 *chunks, const uint32_t *n_chunks, BoundParams bp,
+    Item *items, const int64_t *wg_off, uint32_t *wg_cnt, const uint8_t *defer, uint32_t G1) {
+    using L = ChunkLayout<KeyT, Item>;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    PhaseTimer clk;
+    timer_start(bp, clk);
+    const uint32_t nch = __builtin_amdgcn_readfirstlane(*n_chunks);
+    ChunkShared *sh = reinterpret_cast<ChunkShared *>(smem + L::SH);
+    clear_tables<KeyT, Item>(smem);
+    if (threadIdx.x == 0) {
+        sh->bump = 0;
+        sh->bump2 = kMcppBase;
+        sh->npair = 0;
+        sh->npid = 0;
+    }
+    R r[kRPT], rn[kRPT];
+    for (uint32_t g = blockIdx.x; g < G1; g += gridDim.x) {
+        __syncthreads();
+        if (threadIdx.x == 0) sh->nitems = wg_cnt[g];
+        bool any = false;
+        for (uint32_t w = g; w < nch; w += G1) {
+            if (!__builtin_amdgcn_readfirstlane((int)defer[w])) continue;  // one flag per chunk
+            any = true;
+            const uint4 d = make_uint4(__builtin_amdgcn_readfirstlane(chunks[w].x),
+                                       __builtin_amdgcn_readfirstlane(chunks[w].y),
+                                       __builtin_amdgcn_readfirstlane(chunks[w].z),
+                                       __builtin_amdgcn_readfirstlane(chunks[w].w));
+            const uint32_t n = d.y & kChunkCount;
+            const R *b = chunk_base(d, recs, refined);
+#pragma unroll
+            for (int k = 0; k < kRPT; ++k) r[k] = b[min((uint32_t)(threadIdx.x + k * kBT), n - 1)];
+            __syncthreads();
+            bound_chunk<KeyT, Item, R>(r, n, d.z, d.w, b, 0u, rn, smem, bp, items + wg_off[g], clk);
+        }
+        __syncthreads();
+        if (any && threadIdx.x == 0) wg_cnt[g] = sh->nitems;
+    }
+    timer_flush(bp, clk);
+}
+
 // wg_rec[g] = records of the chunks workgroup g of G will process (w = g mod G)
 __global__ __launch_bounds__(256) void k_wg_records(const uint4 *chunks, const uint32_t *n_chunks,
                                                     uint32_t G, uint32_t *wg_rec) {

@@ -139,10 +139,18 @@ constexpr int kMidWPS = 4;
 template <class R>
 constexpr bool kHasMid = kNarrowCand<R> < kMidCand;
 constexpr int kWideWPS = 2;
+// tier 3: medium chunks (one fine bucket of kWCap + 1 .. capM records),
+// streamed (stream_bound_chunk below) with the narrow pass's working set
 template <class R, int kTier>
-constexpr int kTierCand = kTier == 0 ? (int)kNarrowCand<R> : kTier == 1 ? (int)kMidCand : kWCap;
+constexpr int kTierCand = kTier == 0 || kTier == 3 ? (int)kNarrowCand<R> : kTier == 1 ? (int)kMidCand : kWCap;
 template <class R, int kTier>
-constexpr int kTierWPS = kTier == 0 ? kNarrowWPS<R> : kTier == 1 ? kMidWPS : kWideWPS;
+constexpr int kTierWPS = kTier == 0 || kTier == 3 ? kNarrowWPS<R> : kTier == 1 ? kMidWPS : kWideWPS;
+// candidate records aimed at per privacy id of more than kStreamBig records in
+// a streamed chunk: up to kStreamMul x cand_mul, at most half the working set
+// (a pid's records crowd into its few Zipf-heavy pairs, so cand_mul records
+// -- ~mpc pairs at one record per pair -- would restart most such pids)
+constexpr uint32_t kStreamBig = 256;
+constexpr float kStreamMul = 4.0f;
 #ifndef DPG_SORT_VREG
 #define DPG_SORT_VREG 0  // bound parameters the narrow kernel keeps in VGPRs (0, 1 or 2 groups; 5 waves per SIMD: 0, r5z)
 #endif
@@ -784,6 +792,130 @@ __device__ __forceinline__ bool sort_bound_chunk(const R (&r0)[kWRPT], const R *
     return st == kRoundDefer;
 }
 
+// One round over a medium chunk (n > kWCap records of one fine bucket, <= 128
+// pid slots) in pieces of kWCap records, re-read from memory (L2-hot after
+// the first pass): (first round only) records per pid slot over every piece,
+// then pid hashes and candidate bounds; then the candidates of every piece
+// compacted into LDS -- the working set holds the candidates, never the
+// chunk.  Returns as sort_round; kRoundDefer when more than kC candidates
+// pass (the chunk is left to the hash-table kernel).
+template <class Item, class R, bool kFirst, bool kWPk, int kC>
+__device__ __forceinline__ int stream_round(const R *base, uint32_t n, uint32_t d1, uint32_t hbase,
+                                            char *smem, const BoundParams &bp, Item *items,
+                                            uint32_t &nitems, PhaseTimer &clk) {
+    using L = SortLayout<Item, R, kWPk, kC>;
+    uint32_t *pidv = reinterpret_cast<uint32_t *>(smem + L::PIDV);
+    uint32_t *pidc = reinterpret_cast<uint32_t *>(smem + L::PIDC);
+    uint32_t *cbnd = reinterpret_cast<uint32_t *>(smem + L::CBND);
+    uint64_t *ckey = reinterpret_cast<uint64_t *>(smem + L::CK);
+    uint32_t *cidx = reinterpret_cast<uint32_t *>(smem + L::CIDX);
+    uint8_t *cpkl = reinterpret_cast<uint8_t *>(smem + L::CPKL);
+    uint32_t *olist = reinterpret_cast<uint32_t *>(smem + L::PSTART);
+    const uint32_t lane = __lane_id();
+    const Fmt f = bp.fmt;
+    const uint32_t pkb = f.pkbits;
+    const uint64_t pkmask = (1ull << pkb) - 1ull;
+    const uint32_t hshift = f.kbits - f.b1;
+    const uint32_t pksh = kWPk ? pkb - kSkPkBits : 0u;
+    auto load = [&](uint32_t p0, uint32_t m, R (&r)[kWRPT]) {
+#pragma unroll
+        for (int k = 0; k < kWRPT; ++k) r[k] = base[p0 + min(lane + 64u * k, m - 1)];
+    };
+    if constexpr (kFirst) {
+        for (uint32_t p0 = 0; p0 < n; p0 += kWCap) {
+            const uint32_t m = min(n - p0, (uint32_t)kWCap);
+            R r[kWRPT];
+            load(p0, m, r);
+#pragma unroll
+            for (int k = 0; k < kWRPT; ++k) {
+                const uint32_t q = ((uint32_t)(RecOps<R>::key(r[k], f) >> pkb) - hbase) & (kWCq - 1);
+                if (lane + 64u * k < m) atomicAdd(&pidc[q], 1u);
+            }
+        }
+        wave_sync();
+        const float cmul = bp.cand_mul;
+        const float big = fmaxf(cmul, fminf(kStreamMul * cmul, 0.5f * (float)kC));
+        uint32_t nocc = 0;
+#pragma unroll
+        for (int j = 0; j < (int)(kWCq / 64); ++j) {
+            const uint32_t qq = lane + 64u * j;
+            const bool occ = pidc[qq] > 0;
+            const uint64_t bo = __ballot(occ);
+            if (occ) olist[nocc + lanes_below(bo)] = qq;
+            nocc += (uint32_t)__popcll(bo);
+        }
+        wave_sync();
+        for (uint32_t o = 0; o < nocc; o += 64) {
+            if (o + lane < nocc) {
+                const uint32_t qq = olist[o + lane];
+                pidv[qq] = pid_hash(bp.seed, (uint64_t)(bp.pid_min + (int64_t)hk_inv(
+                                                            (d1 << hshift) | (hbase + qq), bp.hash)));
+                const uint32_t rc = pidc[qq];
+                const float fr = (rc > kStreamBig ? big : cmul) / (float)rc;
+                cbnd[qq] = rc <= bp.mpc || fr >= 1.0f ? 0xFFFFFFFFu : (uint32_t)(fr * 4294967296.0f);
+            }
+        }
+        wave_sync();
+    }
+    uint32_t nc = 0;
+    for (uint32_t p0 = 0; p0 < n; p0 += kWCap) {
+        const uint32_t m = min(n - p0, (uint32_t)kWCap);
+        R r[kWRPT];
+        load(p0, m, r);
+#pragma unroll
+        for (int k = 0; k < kWRPT; ++k) {
+            const uint64_t key = RecOps<R>::key(r[k], f);
+            const uint32_t q = ((uint32_t)(key >> pkb) - hbase) & (kWCq - 1);
+            const uint32_t pk = (uint32_t)(key & pkmask);
+            const uint32_t pp = pair_prio_h(pidv[q], pk);
+            uint64_t sk = ((uint64_t)q << 56) | (uint64_t)(kWPk ? (pk >> pksh) : pk);
+            sk |= (uint64_t)pp << kSkPkBits;
+            const bool c = lane + 64u * k < m && pp <= cbnd[q];
+            const uint64_t bc = __ballot(c);
+            const uint32_t e = nc + lanes_below(bc);
+            if (c && e < L::CAP) {
+                ckey[e] = sk;
+                cidx[e] = RecOps<R>::idx(r[k], f);
+                if constexpr (kWPk) cpkl[e] = (uint8_t)(pk & ((1u << pksh) - 1u));
+            }
+            nc += (uint32_t)__popcll(bc);
+        }
+    }
+    wave_sync();
+    mark(bp, 0, clk);
+    if (nc > (uint32_t)kC) return kRoundDefer;
+    constexpr bool last = !kFirst;
+    int st;
+    if (nc <= 64)
+        st = sort_chunk<Item, R, 1, kWPk, false, L::CAP>(nc, smem, bp, last, 0u, 0u, items, nitems, clk);
+    else if (nc <= 128)
+        st = sort_chunk<Item, R, 2, kWPk, false, L::CAP>(nc, smem, bp, last, 0u, 0u, items, nitems, clk);
+    else
+        st = sort_chunk<Item, R, 4, kWPk, false, L::CAP>(nc, smem, bp, last, 0u, 0u, items, nitems, clk);
+    wave_sync();
+    return st;
+}
+
+// One medium chunk by stream_round (a second round when a filtered pid is
+// short of mpc candidate pairs).  Returns true when the chunk was deferred
+// (nothing emitted: a restart or a deferral happens before any item).
+template <class Item, class R, bool kWPk, int kC>
+__device__ __forceinline__ bool stream_bound_chunk(const R *base, uint32_t n, uint32_t d1,
+                                                   uint32_t hbase, char *smem, const BoundParams &bp,
+                                                   Item *items, uint32_t &nitems, PhaseTimer &clk) {
+    using L = SortLayout<Item, R, kWPk, kC>;
+    uint32_t *pidc = reinterpret_cast<uint32_t *>(smem + L::PIDC);
+    const uint32_t lane = __lane_id();
+    int st = stream_round<Item, R, true, kWPk, kC>(base, n, d1, hbase, smem, bp, items, nitems, clk);
+    if (st == kRoundRestart)
+        st = stream_round<Item, R, false, kWPk, kC>(base, n, d1, hbase, smem, bp, items, nitems, clk);
+#pragma unroll
+    for (int j = 0; j < (int)(kWCq / 64); ++j) pidc[lane + 64u * j] = 0;
+    wave_sync();
+    mark(bp, 5, clk);
+    return st == kRoundDefer;
+}
+
 // Persistent single-wave workgroups walk the small-chunk list statically
 // (w, w + G1, ...), as k_bound_waves; narrow workgroup g appends its items
 // to items[wg_off[g], ...) and leaves the count in wg_cnt[g], and flags the
@@ -882,6 +1014,19 @@ __global__ __launch_bounds__(64, (kTierWPS<R, kTier>)) void k_bound_sorted(
 #pragma unroll
                 for (int k = 0; k < kWRPT; ++k) r[k] = nb[min(lane + 64u * k, nn - 1)];
             }
+        }
+        if (lane == 0) wg_cnt[blockIdx.x] = nitems;
+    } else if constexpr (kTier == 3) {
+        // the medium-chunk list, statically (w, w + G, ...); workgroup g
+        // appends to items[wg_off[g], ...) and flags the chunks it defers
+        uint32_t nitems = 0;
+        Item *my_items = items + wg_off[blockIdx.x];
+        for (uint32_t w = blockIdx.x; w < nch; w += gridDim.x) {
+            const uint4 d = desc(w);
+            const bool df = stream_bound_chunk<Item, R, kWPk, kC>(
+                wave_chunk_base(d, recs, refined, heavy), d.y & kChunkCount, d.z & 0xFFFFu, d.w,
+                smem, bp, my_items, nitems, clk);
+            if (lane == 0) defer[w] = df ? 1 : 0;
         }
         if (lane == 0) wg_cnt[blockIdx.x] = nitems;
     } else {

@@ -441,22 +441,27 @@ MW_MODES = [m for m in MODES if m[0] in ("cross_and_per", "mean_var", "count_onl
 
 
 @pytest.mark.parametrize("name,kw", MW_MODES, ids=[m[0] for m in MW_MODES])
-@pytest.mark.parametrize("mw", ["multiwave", "default", "single"])
+@pytest.mark.parametrize("mw", ["multiwave", "default", "single", "hash_medium"])
 def test_gpu_wide_and_medium_chunks_match_oracle(built, monkeypatch, name, kw, mw):
     """Chunks of more than 256 candidate records (two 200-record privacy ids
     per chunk, mpc 100: the pre-filter passes almost everything) and medium
     chunks (one 700-record privacy id per fine bucket) through the
     multi-wave sort kernels (dpg_sortmw.h: 2 waves per wide chunk, 4 per
     medium chunk) -- and, DPG_MW_OFF, through the single-wave 8-element
-    kernel and the hash-table medium kernel -- keep exactly the oracle's
-    records.  The default is the 2-wave wide kernel with the hash-table
-    medium kernel (DPG_MW_MEDIUM=1 adds the 4-wave one)."""
+    kernel -- keep exactly the oracle's records.  The default is the 2-wave
+    wide kernel with the streamed single-wave medium pass (dpg_sortb.h tier
+    3), whose chunks of too many candidates (here: most, at mpc 100) go to
+    the hash-table medium kernel; DPG_MEDIUM_STREAM=0 gives every medium
+    chunk to the hash-table kernel, DPG_MW_MEDIUM=1 to the 4-wave one."""
     monkeypatch.delenv("DPG_MW_OFF", raising=False)
     monkeypatch.delenv("DPG_MW_MEDIUM", raising=False)
+    monkeypatch.delenv("DPG_MEDIUM_STREAM", raising=False)
     if mw == "single":
         monkeypatch.setenv("DPG_MW_OFF", "1")
     elif mw == "multiwave":
         monkeypatch.setenv("DPG_MW_MEDIUM", "1")
+    elif mw == "hash_medium":
+        monkeypatch.setenv("DPG_MEDIUM_STREAM", "0")
     rng = np.random.default_rng(77)
     P = 2000
     pid = np.concatenate([np.repeat(np.arange(6000), 200), np.repeat(np.arange(6000, 6300), 700)])
@@ -476,7 +481,53 @@ def test_gpu_wide_and_medium_chunks_match_oracle(built, monkeypatch, name, kw, m
     res.materialize()
     st = backend.ctx.stage_times()
     assert ("bound.multiwave" in st) == (mw != "single")
+    assert ("bound.medium_deferred" in st) == (mw in ("default", "single"))
     assert st["bound.wide"] > 0.0 and st["bound.medium"] > 0.0
+    plan = res.plan
+    ref = oracle.bound_aggregate(pid, pk, val if plan.needs_values() else None,
+                                 res.last_bound_fields, SEED, public_mask=oracle.bitmap(range(P), P))
+    got = {k: (v.cpu().numpy() if v is not None else None) for k, v in res.last_partials.items()}
+    assert np.array_equal(got["rows"], ref["rows"])
+    assert np.array_equal(got["count"], ref["count"])
+    for k in ("sum", "nsum", "nsq"):
+        if got[k] is not None:
+            assert np.allclose(got[k], ref[k], rtol=1e-9, atol=1e-9), k
+
+
+@pytest.mark.parametrize("name,kw", MW_MODES, ids=[m[0] for m in MW_MODES])
+@pytest.mark.parametrize("size", [600, 1000])
+def test_gpu_streamed_medium_chunks_match_oracle(built, monkeypatch, name, kw, size):
+    """Medium chunks streamed by single waves (dpg_sortb.h tier 3): one
+    privacy id of `size` records per fine bucket, mpc 8, so ~84 candidate
+    records each; one id in ten puts its records into three partitions (its
+    candidates show fewer than mpc pairs: a restart with the bound lifted,
+    then more candidates than the working set holds, so the chunk goes to
+    the hash-table kernel).  Partials equal the oracle's."""
+    monkeypatch.delenv("DPG_MW_MEDIUM", raising=False)
+    monkeypatch.delenv("DPG_MEDIUM_STREAM", raising=False)
+    rng = np.random.default_rng(size)
+    P = 20_000
+    n_pid = 1500
+    pid = np.repeat(np.arange(n_pid), size)
+    pk = ((rng.zipf(1.1, pid.size) - 1) % P).astype(np.int64)
+    few = np.isin(pid, np.arange(0, n_pid, 10))
+    pk[few] = rng.integers(0, 3, int(few.sum())) * 7
+    perm = rng.permutation(pid.size)
+    pid, pk = pid[perm].astype(np.int64), pk[perm]
+    val = rng.uniform(-2.0, 12.0, pid.size)
+    kw = dict(kw, max_partitions_contributed=8, max_contributions_per_partition=2)
+    params = pdp.AggregateParams(**kw)
+    backend = pdp.MI355XBackend(device=0, seed=SEED)
+    acc = pdp.NaiveBudgetAccountant(1.0, 1e-6)
+    res = pdp.DPEngine(acc, backend).aggregate(
+        pdp.ColumnarData(pid=torch.as_tensor(pid), pk=torch.as_tensor(pk),
+                         value=torch.as_tensor(val), n_partitions=P),
+        params, pdp.DataExtractors("pid", "pk", "value"), public_partitions=list(range(P)))
+    acc.compute_budgets()
+    res.noise_enabled = False
+    res.materialize()
+    st = backend.ctx.stage_times()
+    assert "bound.medium_deferred" in st
     plan = res.plan
     ref = oracle.bound_aggregate(pid, pk, val if plan.needs_values() else None,
                                  res.last_bound_fields, SEED, public_mask=oracle.bitmap(range(P), P))
