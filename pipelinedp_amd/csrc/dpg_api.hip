@@ -675,13 +675,16 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     if (hctl.err & 8u) return kRedoLevel2;
     uint4 *chunk_list = chunks;
     size_t chunk_cap = B;  // entries of chunk_list
-    const uint4 *mchunk_list = mchunks;
+    uint4 *mchunk_list = mchunks;
     const R *refined = recs;
     // global-memory leftovers: (buffer, starts, counts, level-1 buckets, number)
     const R *g_base = recs;
     const int64_t *g_start = ostart;
     const uint32_t *g_cnt = ocnt;
     const uint32_t *g_d1 = od1;
+    const uint32_t *g_hb = ohb;
+    unsigned long long g_records = hctl.over_records;
+    uint32_t g_plb = pl.plb;  // pid hash bits below an oversize bucket
     uint32_t n_global = 0;
     if (hctl.n_over > 0) {
         const uint32_t rbits = std::min<uint32_t>(kMaxBR, pl.plb);  // hash bits not yet used
@@ -736,6 +739,9 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
             g_start = o2start;
             g_cnt = o2cnt;
             g_d1 = o2d1;
+            g_hb = o2hb;
+            g_records = hctl.over2_records;
+            g_plb = plb2;
             n_global = hctl.n_over2;
         }
     }
@@ -746,9 +752,48 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     const bool per_pid = bp.mode == DPG_MODE_PER_PRIVACY_ID;
     const bool heavy = n_global > 0 && !per_pid && !ItemTraits<Item>::preagg && bp.mpc <= 128 &&
                        std::getenv("DPG_NO_HEAVY") == nullptr;
+    // the cross-partition modes sort (dpg_sortb.h) when the partition key
+    // fits the sort key; PER_PRIVACY_ID, the pre-aggregate and wider keys
+    // take the hash-table kernel (dpg_wave.h).  DPG_BOUND_HASH: force it.
+    bool use_sort = false;
+    if constexpr (!ItemTraits<Item>::preagg)
+        use_sort = !per_pid && std::getenv("DPG_BOUND_HASH") == nullptr &&
+                   (pl.pkbits <= kSkPkBits || (sizeof(R) == 12 && pl.pkbits <= 32));
+    // medium chunks: streamed by single waves of the sort kernel (tier 3,
+    // the narrow pass's working set), the chunks it defers by the hash-table
+    // kernel; DPG_MEDIUM_STREAM=0 (or DPG_MW_MEDIUM): the workgroup kernels
+    // alone.  Pid slots need <= 7 hash bits below a bucket.
+    const char *ms_env = std::getenv("DPG_MEDIUM_STREAM");
+    const bool stream_ok = use_sort && pl.plb <= 7 && !(ms_env && std::atoi(ms_env) == 0) &&
+                           std::getenv("DPG_MW_MEDIUM") == nullptr;
+    // ... and the oversize buckets join the medium list instead of the heavy
+    // filter: the streamed pass holds candidates, never a chunk, so size does
+    // not matter; an oversize chunk it cannot bound goes back to the
+    // global-memory kernel (heavy_fb, as the heavy chunks' do).
+    // Only while the pass aims at its full kStreamMul x cand_mul candidates
+    // per big privacy id (mpc <= ~13): with a capped aim (config 4, mpc 50)
+    // the kept pairs often include a Zipf-heavy pair of more records than
+    // the working set holds, and a handed-back bucket costs the global-memory
+    // kernel (same-box A/B: config 4 75.6 -> 92.6 ms, bound.tail 18 ms;
+    // (1e9, 1e6), mpc 8: 21.7 -> 18.5 ms).  DPG_STREAM_OVER=0: the heavy
+    // filter always, =1: the streamed pass always.
+    const char *so_env = std::getenv("DPG_STREAM_OVER");
+    const bool so_aim = bp.cand_mul * kStreamMul <= 0.5f * (float)kNarrowCand<R>;
+    const bool stream_over = heavy && stream_ok &&
+                             (so_env ? std::atoi(so_env) != 0 : so_aim);
+    uint32_t n_m0 = 0xFFFFFFFFu;  // first oversize entry of the medium list (none)
     const R *hrec = recs;
     uint32_t *hfb = nullptr;
-    if (heavy) {
+    if (stream_over) {
+        WS(hf, uint32_t, "heavy.fb", n_global);
+        hfb = hf;
+        n_m0 = hctl.n_mchunks;
+        k_over_to_medium<<<(n_global + 255) / 256, 256, 0, s>>>(
+            g_start, g_cnt, g_d1, g_hb, n_global, g_base == recs ? 0u : 1u, mchunk_list,
+            &ctl->n_mchunks, n_m0);
+        LAUNCH_CHECK();
+        hctl.n_mchunks += n_global;
+    } else if (heavy) {
         stage(ctx, s, "heavy");
         WS(hr, R, "heavy.recs", (size_t)n_global * kWCap);
         WS(hf, uint32_t, "heavy.fb", n_global);
@@ -767,15 +812,8 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     // writes its items to items[wg_off[g], ...)
     // one kernel per bounding family (PER_PRIVACY_ID or cross-partition), so
     // that the hot one holds one path only
-    // the cross-partition modes sort (dpg_sortb.h) when the partition key
-    // fits the sort key; PER_PRIVACY_ID, the pre-aggregate and wider keys
-    // take the hash-table kernel (dpg_wave.h).  DPG_BOUND_HASH: force it.
     auto wave_kern = per_pid ? k_bound_waves<KeyT, Item, R, true> : k_bound_waves<KeyT, Item, R, false>;
     size_t wave_lds = WL::TOTAL;
-    bool use_sort = false;
-    if constexpr (!ItemTraits<Item>::preagg)
-        use_sort = !per_pid && std::getenv("DPG_BOUND_HASH") == nullptr &&
-                   (pl.pkbits <= kSkPkBits || (sizeof(R) == 12 && pl.pkbits <= 32));
     // partition keys wider than the sort key's 24 bits: the wide-key kernels
     // (their low bits ride in the sort payload; 12-byte records only)
     const bool wpk = pl.pkbits > kSkPkBits;
@@ -835,14 +873,7 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     const int per_cu = use_sort ? waves_per_cu(narrow, wave_lds, 4 * kNarrowWPS<R>)
                                 : waves_per_cu((const void *)wave_kern, wave_lds);
     const uint32_t Gw = (uint32_t)(ctx->n_cu * per_cu);
-    // medium chunks: streamed by single waves of the sort kernel (tier 3,
-    // the narrow pass's working set), the chunks it defers by the hash-table
-    // kernel; DPG_MEDIUM_STREAM=0 (or DPG_MW_MEDIUM): the workgroup kernels
-    // alone.  Pid slots need <= 7 hash bits below a bucket.
-    const char *ms_env = std::getenv("DPG_MEDIUM_STREAM");
-    const bool stream_med = medium != nullptr && hctl.n_mchunks > 0 && pl.plb <= 7 &&
-                            !(ms_env && std::atoi(ms_env) == 0) &&
-                            std::getenv("DPG_MW_MEDIUM") == nullptr;
+    const bool stream_med = medium != nullptr && hctl.n_mchunks > 0 && stream_ok;
     const uint32_t Gm =
         !hctl.n_mchunks ? 0u
         : stream_med    ? (uint32_t)std::min<uint32_t>(
@@ -851,7 +882,14 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
                         : (uint32_t)std::min<uint32_t>(ctx->n_cu * CL::PER_CU, hctl.n_mchunks);
     const uint32_t G = Gw + Gm;
     // heavy buckets handed back are counted twice (candidates + bucket)
-    const int64_t items_cap = std::max<int64_t>(n + (heavy ? (int64_t)n_global * kWCap : 0), 1);
+    // streamed oversize buckets handed back emit behind the regions of the
+    // chunk lists: <= mpc items per privacy id (one per bucket when no hash
+    // bits are left below it), else <= its records
+    const int64_t hv_extra =
+        !heavy        ? 0
+        : stream_over ? (g_plb == 0 ? (int64_t)n_global * bp.mpc : (int64_t)g_records)
+                      : (int64_t)n_global * kWCap;
+    const int64_t items_cap = std::max<int64_t>(n + hv_extra, 1);
     WS(items, Item, "items", items_cap);
     WS(wg_rec, uint32_t, "wg.rec", G + 1);
     WS(wg_off, int64_t, "wg.off", G + 2);
@@ -956,7 +994,7 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
                 constexpr bool W = decltype(wpk_tag)::value;
                 k_bound_sorted<Item, R, 3, W><<<Gm, 64, wave_lds, s>>>(
                     recs, refined, recs, mchunk_list, &ctl->n_mchunks, bpm, items, wg_off + Gw,
-                    wg_cnt + Gw, mdefer, Gm);
+                    wg_cnt + Gw, mdefer, n_m0);
             };
             if (!wpk) {
                 launch_s(std::false_type{});

@@ -684,6 +684,17 @@ __global__ __launch_bounds__(kBT) void k_bound_chunks_deferred(
     timer_flush(bp, clk);
 }
 
+// Oversize buckets (start, count, level-1 bucket, residual base) appended to
+// the medium-chunk list behind its n_m0 entries (sel: the buffer they live
+// in), for the streamed sort pass (dpg_sortb.h tier 3).
+__global__ void k_over_to_medium(const int64_t *st, const uint32_t *cnt, const uint32_t *d1,
+                                 const uint32_t *hb, uint32_t n, uint32_t sel, uint4 *mchunks,
+                                 uint32_t *n_mchunks, uint32_t n_m0) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) mchunks[n_m0 + i] = make_uint4((uint32_t)st[i], cnt[i] | (sel << 31), d1[i], hb[i]);
+    if (i == 0) *n_mchunks = n_m0 + n;
+}
+
 // wg_rec[g] = records of the chunks workgroup g of G will process (w = g mod G)
 __global__ __launch_bounds__(256) void k_wg_records(const uint4 *chunks, const uint32_t *n_chunks,
                                                     uint32_t G, uint32_t *wg_rec) {

@@ -1018,7 +1018,9 @@ __global__ __launch_bounds__(64, (kTierWPS<R, kTier>)) void k_bound_sorted(
         if (lane == 0) wg_cnt[blockIdx.x] = nitems;
     } else if constexpr (kTier == 3) {
         // the medium-chunk list, statically (w, w + G, ...); workgroup g
-        // appends to items[wg_off[g], ...) and flags the chunks it defers
+        // appends to items[wg_off[g], ...) and flags the chunks it defers --
+        // except entries w >= G1, oversize buckets (k_over_to_medium), which
+        // go back to the global-memory kernel as oversize bucket w - G1
         uint32_t nitems = 0;
         Item *my_items = items + wg_off[blockIdx.x];
         for (uint32_t w = blockIdx.x; w < nch; w += gridDim.x) {
@@ -1026,7 +1028,11 @@ __global__ __launch_bounds__(64, (kTierWPS<R, kTier>)) void k_bound_sorted(
             const bool df = stream_bound_chunk<Item, R, kWPk, kC>(
                 wave_chunk_base(d, recs, refined, heavy), d.y & kChunkCount, d.z & 0xFFFFu, d.w,
                 smem, bp, my_items, nitems, clk);
-            if (lane == 0) defer[w] = df ? 1 : 0;
+            if (lane == 0) {
+                const bool over = w >= G1;
+                if (df && over) bp.heavy_fb[atomicAdd(bp.heavy_nfb, 1u)] = w - G1;
+                defer[w] = df && !over ? 1 : 0;
+            }
         }
         if (lane == 0) wg_cnt[blockIdx.x] = nitems;
     } else {

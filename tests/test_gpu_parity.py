@@ -537,3 +537,51 @@ def test_gpu_streamed_medium_chunks_match_oracle(built, monkeypatch, name, kw, s
     for k in ("sum", "nsum", "nsq"):
         if got[k] is not None:
             assert np.allclose(got[k], ref[k], rtol=1e-9, atol=1e-9), k
+
+
+@pytest.mark.parametrize("name,kw", MW_MODES, ids=[m[0] for m in MW_MODES])
+@pytest.mark.parametrize("over", ["stream", "heavy_filter"])
+def test_gpu_oversize_buckets_match_oracle(built, monkeypatch, name, kw, over):
+    """Oversize buckets (a 64-record bucket capacity, dpg_set_tuning; one
+    privacy id of ~100 records per bucket): streamed by the sort pass's
+    tier 3 from the medium list (default) or cut by the heavy filter into
+    heavy chunks (DPG_STREAM_OVER=0).  One id in ten puts its records into
+    three partitions: the streamed pass hands its bucket back to the
+    global-memory kernel.  Partials equal the oracle's."""
+    monkeypatch.delenv("DPG_NO_HEAVY", raising=False)
+    monkeypatch.delenv("DPG_MEDIUM_STREAM", raising=False)
+    monkeypatch.delenv("DPG_MW_MEDIUM", raising=False)
+    monkeypatch.setenv("DPG_STREAM_OVER", "1" if over == "stream" else "0")
+    rng = np.random.default_rng(404)
+    P = 3000
+    n_pid = 2000
+    pid = rng.integers(0, n_pid, 200_000)
+    pk = ((rng.zipf(1.1, pid.size) - 1) % P).astype(np.int64)
+    few = pid % 10 == 3
+    pk[few] = rng.integers(0, 3, int(few.sum())) * 11
+    pid = pid.astype(np.int64)
+    val = rng.uniform(-2.0, 12.0, pid.size)
+    kw = dict(kw, max_partitions_contributed=4, max_contributions_per_partition=2)
+    params = pdp.AggregateParams(**kw)
+    backend = pdp.MI355XBackend(device=0, seed=SEED)
+    backend.ctx.set_tuning(1024, 64)
+    acc = pdp.NaiveBudgetAccountant(1.0, 1e-6)
+    res = pdp.DPEngine(acc, backend).aggregate(
+        pdp.ColumnarData(pid=torch.as_tensor(pid), pk=torch.as_tensor(pk),
+                         value=torch.as_tensor(val), n_partitions=P),
+        params, pdp.DataExtractors("pid", "pk", "value"), public_partitions=list(range(P)))
+    acc.compute_budgets()
+    res.noise_enabled = False
+    res.materialize()
+    st = backend.ctx.stage_times()
+    assert ("heavy" in st) == (over == "heavy_filter")
+    assert "bound.medium" in st
+    plan = res.plan
+    ref = oracle.bound_aggregate(pid, pk, val if plan.needs_values() else None,
+                                 res.last_bound_fields, SEED, public_mask=oracle.bitmap(range(P), P))
+    got = {k: (v.cpu().numpy() if v is not None else None) for k, v in res.last_partials.items()}
+    assert np.array_equal(got["rows"], ref["rows"])
+    assert np.array_equal(got["count"], ref["count"])
+    for k in ("sum", "nsum", "nsq"):
+        if got[k] is not None:
+            assert np.allclose(got[k], ref[k], rtol=1e-9, atol=1e-9), k
