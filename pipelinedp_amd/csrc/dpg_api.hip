@@ -613,6 +613,11 @@ BoundParams to_bound(const dpg_bound_params *p, uint64_t seed) {
     float cc = kSortCandC;
     if (const char *e = std::getenv("DPG_SORT_CAND_C")) cc = (float)std::atof(e);
     b.cand_mul = cc * ((float)b.mpc + 2.0f * std::sqrt((float)b.mpc) + 2.0f);
+    // expected candidates past which the narrow / streamed passes defer a
+    // chunk before drawing its pair priorities (1.25 x their 256-candidate
+    // working set; DPG_EARLY_DEFER=0: off)
+    const char *ed = std::getenv("DPG_EARLY_DEFER");
+    b.defer_est = (ed && std::atoi(ed) == 0) ? 0.0f : 1.25f * 256.0f;
     return b;
 }
 

@@ -48,6 +48,9 @@ struct BoundParams {
     uint32_t *heavy_fb;    // heavy buckets handed back to k_bound_big (indices)
     uint32_t *heavy_nfb;   // their number
     float cand_mul;        // sort kernel: candidate records aimed at per filtered pid
+    float defer_est;       // sort kernel, narrow / streamed passes: a chunk whose
+                           // expected candidates exceed this is deferred before
+                           // its pair priorities are drawn (0: off)
 };
 
 // privacy id of a bucket's pid-hash residual

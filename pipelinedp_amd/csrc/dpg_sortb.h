@@ -696,6 +696,7 @@ __device__ __forceinline__ int sort_round(const R (&r)[kWRPT], uint32_t n, uint3
             nocc += (uint32_t)__popcll(bo);
         }
         wave_sync();
+        float est = 0.0f;  // expected candidates: all records of unfiltered pids, ~cmul of the others
         for (uint32_t o = 0; o < nocc; o += 64) {
             if (o + lane < nocc) {
                 const uint32_t qq = olist[o + lane];
@@ -703,12 +704,19 @@ __device__ __forceinline__ int sort_round(const R (&r)[kWRPT], uint32_t n, uint3
                                                             (d1 << hshift) | (hbase + qq), bp.hash)));
                 const uint32_t rc = pidc[qq];
                 const float fr = cmul / (float)rc;
-                cbnd[qq] = hbound ? hbound
-                                  : (rc <= bp.mpc || fr >= 1.0f ? 0xFFFFFFFFu
-                                                                : (uint32_t)(fr * 4294967296.0f));
+                const bool all = hbound || rc <= bp.mpc || fr >= 1.0f;
+                cbnd[qq] = hbound ? hbound : all ? 0xFFFFFFFFu : (uint32_t)(fr * 4294967296.0f);
+                est += all ? (float)rc : cmul;
             }
         }
         wave_sync();
+        if constexpr (!kWide) {
+            // a chunk that will hold more candidates than the working set goes
+            // to the wide pass before its priorities are drawn
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) est += __shfl_xor(est, o, 64);
+            if (bp.defer_est > 0.0f && est > bp.defer_est) return kRoundDefer;
+        }
     }
     uint32_t nc = 0;
     {
@@ -845,17 +853,24 @@ __device__ __forceinline__ int stream_round(const R *base, uint32_t n, uint32_t 
             nocc += (uint32_t)__popcll(bo);
         }
         wave_sync();
+        float est = 0.0f;  // expected candidates (see sort_round)
         for (uint32_t o = 0; o < nocc; o += 64) {
             if (o + lane < nocc) {
                 const uint32_t qq = olist[o + lane];
                 pidv[qq] = pid_hash(bp.seed, (uint64_t)(bp.pid_min + (int64_t)hk_inv(
                                                             (d1 << hshift) | (hbase + qq), bp.hash)));
                 const uint32_t rc = pidc[qq];
-                const float fr = (rc > kStreamBig ? big : cmul) / (float)rc;
-                cbnd[qq] = rc <= bp.mpc || fr >= 1.0f ? 0xFFFFFFFFu : (uint32_t)(fr * 4294967296.0f);
+                const float aim = rc > kStreamBig ? big : cmul;
+                const float fr = aim / (float)rc;
+                const bool all = rc <= bp.mpc || fr >= 1.0f;
+                cbnd[qq] = all ? 0xFFFFFFFFu : (uint32_t)(fr * 4294967296.0f);
+                est += all ? (float)rc : aim;
             }
         }
         wave_sync();
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) est += __shfl_xor(est, o, 64);
+        if (bp.defer_est > 0.0f && est > bp.defer_est) return kRoundDefer;
     }
     uint32_t nc = 0;
     for (uint32_t p0 = 0; p0 < n; p0 += kWCap) {
