@@ -652,8 +652,11 @@ int bound_and_reduce(dpg_ctx *ctx, hipStream_t s, const Plan &pl, const R *recs,
     if (const char *e = std::getenv("DPG_DEBUG_CAP"))  // debug: medium-chunk experiments
         capM = std::max<uint32_t>(1, std::min<uint32_t>(capM, (uint32_t)std::atoi(e)));
     // small chunks need <= 7 pid hash bits below a bucket (kWCq = 128 slots)
+    uint32_t capS = (uint32_t)kWCap;
+    if (const char *e = std::getenv("DPG_DEBUG_CAPS"))  // debug: small-chunk packing experiments
+        capS = std::max<uint32_t>(64, std::min<uint32_t>(capS, (uint32_t)std::atoi(e)));
     auto cap_small = [&](uint32_t plb) {
-        return plb <= 7 ? std::min<uint32_t>(capM, (uint32_t)kWCap) : 0u;
+        return plb <= 7 ? std::min<uint32_t>(capM, capS) : 0u;
     };
     const Fmt f = bp.fmt;
     // ---- pack fine buckets into chunks (groups never span level-1 buckets)

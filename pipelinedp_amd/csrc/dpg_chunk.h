@@ -754,12 +754,12 @@ __global__ __launch_bounds__(256) void k_make_chunks(
     uint32_t *n_over, unsigned long long *over_records) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t b0 = g * group;
-    if (b0 >= B) return;
-    const uint32_t b1 = min(B, b0 + group);
+    const bool active = b0 < B;  // every lane takes part in the reservations below
+    const uint32_t b1 = active ? min(B, b0 + group) : b0;
     const uint32_t maxspan = max(1u, kWCq >> plb);
     const uint32_t lmask = (1u << d1_shift) - 1u;
-    const uint32_t d1 = d1_map ? d1_map[b0 >> d1_shift] : (b0 >> d1_shift);
-    const uint32_t hb0 = hb_map ? hb_map[b0 >> d1_shift] : 0u;
+    const uint32_t d1 = !active ? 0u : d1_map ? d1_map[b0 >> d1_shift] : (b0 >> d1_shift);
+    const uint32_t hb0 = active && hb_map ? hb_map[b0 >> d1_shift] : 0u;
     // the group's first kMkPre counts and starts, all loads in flight at
     // once (the two passes below used to load them bucket by bucket: 0.25
     // ms of dependent loads at config 2 for 48 MB); a group of more buckets
@@ -769,15 +769,25 @@ __global__ __launch_bounds__(256) void k_make_chunks(
     int64_t spre[kMkPre];
 #pragma unroll
     for (uint32_t j = 0; j < kMkPre; ++j) {
-        const uint32_t b = min(b0 + j, b1 - 1);
-        cpre[j] = bcnt[b];
-        spre[j] = bstart[b];
+        const uint32_t b = active ? min(b0 + j, b1 - 1) : 0u;
+        cpre[j] = active ? bcnt[b] : 0u;
+        spre[j] = active ? bstart[b] : 0;
     }
-    // pass 1: count small chunks
-    uint32_t nc = 0, cur = 0, bfirst = 0;
+    // pass 1: count small chunks, medium chunks, oversize buckets (records)
+    uint32_t nc = 0, nm = 0, no = 0, cur = 0, bfirst = 0;
+    double orec = 0.0;  // exact: < 2^53
     int64_t cend = -1;
     auto count_step = [&](uint32_t b, uint32_t c, int64_t st) {
-        if (c == 0 || c > capS) return;
+        if (c == 0) return;
+        if (c > capM) {
+            ++no;
+            orec += (double)c;
+            return;
+        }
+        if (c > capS) {
+            ++nm;
+            return;
+        }
         if (cur == 0 || cur + c > capS || st != cend || b - bfirst >= maxspan) {
             ++nc;
             cur = 0;
@@ -790,7 +800,26 @@ __global__ __launch_bounds__(256) void k_make_chunks(
     for (uint32_t j = 0; j < kMkPre; ++j)
         if (b0 + j < b1) count_step(b0 + j, cpre[j], spre[j]);
     for (uint32_t b = b0 + kMkPre; b < b1; ++b) count_step(b, bcnt[b], bstart[b]);
-    uint32_t base = nc ? atomicAdd(n_chunks, nc) : 0;
+    // one reservation per wave and list (per-entry atomics on one counter
+    // serialise in L2: 0.9 ms for config 2's buckets at a 384-record cap)
+    uint32_t tc, tm, to;
+    uint32_t base = wave_excl_scan(nc, tc), mbase = wave_excl_scan(nm, tm),
+             obase = wave_excl_scan(no, to);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) orec += __shfl_xor(orec, o, 64);
+    uint32_t rc = 0, rm = 0, ro = 0;
+    if (__lane_id() == 0) {
+        if (tc) rc = atomicAdd(n_chunks, tc);
+        if (tm) rm = atomicAdd(n_mchunks, tm);
+        if (to) {
+            ro = atomicAdd(n_over, to);
+            atomicAdd(over_records, (unsigned long long)orec);
+        }
+    }
+    base += __builtin_amdgcn_readfirstlane(rc);
+    mbase += __builtin_amdgcn_readfirstlane(rm);
+    obase += __builtin_amdgcn_readfirstlane(ro);
+    if (!active) return;
     // pass 2: write
     cur = 0;
     cend = -1;
@@ -800,16 +829,15 @@ __global__ __launch_bounds__(256) void k_make_chunks(
         if (c == 0) return;
         const uint32_t hb = hb0 + ((b & lmask) << plb);
         if (c > capM) {
-            const uint32_t o = atomicAdd(n_over, 1u);
+            const uint32_t o = obase++;
             over_start[o] = st;
             over_cnt[o] = c;
             over_d1[o] = d1;
             over_hb[o] = hb;
-            atomicAdd(over_records, (unsigned long long)c);
             return;
         }
         if (c > capS) {
-            mchunks[atomicAdd(n_mchunks, 1u)] = make_uint4((uint32_t)st, c | (sel << 31), d1, hb);
+            mchunks[mbase++] = make_uint4((uint32_t)st, c | (sel << 31), d1, hb);
             return;
         }
         if (cur == 0 || cur + c > capS || st != cend || b - bfirst >= maxspan) {

@@ -366,12 +366,15 @@ __device__ __forceinline__ int mw_sort_chunk(uint32_t nc, char *smem, const Boun
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            if (!__ballot((overm >> j) & 1u)) continue;
             const bool ov = (overm >> j) & 1u;
+            // this wave's longest over-full pair in slot j (the sorted
+            // order puts a long pair in few neighbouring threads)
+            const uint32_t mj = __builtin_amdgcn_readfirstlane(wave_max_u32(ov ? len[j] : 0u));
+            if (!mj) continue;
             const uint64_t mine = rks[4 * tid + j];
             const uint32_t lm = max(len[j], 1u) - 1u;
             uint32_t below = 0;
-            for (uint32_t t = 0; t < maxlen; t += 2) {
+            for (uint32_t t = 0; t < mj; t += 2) {
                 const uint64_t y0 = rks[min(st[j] + min(t, lm), (uint32_t)CAP - 1)];
                 const uint64_t y1 = rks[min(st[j] + min(t + 1, lm), (uint32_t)CAP - 1)];
                 below += (t < len[j] && y0 < mine) ? 1u : 0u;
