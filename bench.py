@@ -284,9 +284,20 @@ def _lib_sha() -> str:
         return hashlib.sha256(f.read()).hexdigest()[:16]
 
 
-def _traffic(c4: bool, records: int):
+def _default_workload(args, c4: bool) -> bool:
+    """The workload configs[1] / configs[3] (private) name, which the PMC
+    passes of tools/gpu_r6_final.sh measure (other inputs: no traffic)."""
+    return (args.records == 1_000_000_000 and args.pids == 10_000_000 and
+            args.partitions == (100_000_000 if c4 else 1_000_000) and
+            args.mpc == (50 if c4 else 8) and args.mcpp == (4 if c4 else 2) and
+            not (c4 and args.public) and (not c4 or args.pid_cap == 1000.0))
+
+
+def _traffic(c4: bool, records: int, default: bool = True):
     """PMC HBM bytes per step from profiles/hbm_traffic[_c4].json -- only if
-    that file was measured on this exact libdpg.so build."""
+    that file was measured on this exact libdpg.so build, for this workload."""
+    if not default:
+        return None, "PMC passes measure the default private workload only"
     tfile = os.path.join(ROOT, "profiles", "hbm_traffic_c4.json" if c4 else "hbm_traffic.json")
     if not os.path.exists(tfile):
         return None, "no PMC file"
@@ -601,7 +612,8 @@ def main():
         stage_ms["bounding"] = sum(stage_ms[k] for k in bparts)
     # headline: the whole path (24 B/record over the device time per step)
     achieved = algo_bytes / (dev_ms_max * 1e-3) / 1e9
-    tj, tsrc = _traffic(c4, args.records)
+    dflt = _default_workload(args, c4)
+    tj, tsrc = _traffic(c4, args.records, dflt)
     kernels = {}
     for st, ms in stage_ms.items():
         b = stage_design_bytes(st, args.records, rec_bytes, item_bytes, kept_recs, kept_pairs,
@@ -616,8 +628,10 @@ def main():
                     f"Zipf(1.1) partitions per GPU, MEAN+VARIANCE, Gaussian, "
                     + ("public partitions" if public is not None else "private selection"))
     else:
-        workload = ("configs[1]: 1e9 records / 1e7 privacy ids / 1e6 Zipf(1.1) partitions "
-                    "per GPU, COUNT+SUM+PRIVACY_ID_COUNT, private partition selection")
+        workload = (("configs[1]: " if dflt else "envelope input (not configs[1]): ") +
+                    f"{args.records:.0e} records / {args.pids:.0e} privacy ids / {P:.0e} "
+                    "Zipf(1.1) partitions per GPU, COUNT+SUM+PRIVACY_ID_COUNT, private "
+                    "partition selection")
     line = {
         "metric": METRIC, "value": value, "unit": "records/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
