@@ -168,6 +168,51 @@ __device__ __forceinline__ void cross_wave_step(uint64_t (&k)[4], uint32_t (&o)[
     }
 }
 
+// The same two steps over float64-packed keys alone (bitonic_sort_keys_f64,
+// dpg_sortb.h): one v_min_f64 / v_max_f64 per compare-exchange.
+__device__ __forceinline__ void half_clean_256_f64(uint64_t (&k)[4]) {
+    uint32_t lid = __lane_id();
+    asm volatile("" : "+v"(lid));
+#pragma unroll
+    for (int ls = 7; ls >= 0; --ls) {
+        const int sd = 1 << ls;
+        if (ls < 2) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (j & sd) continue;
+                const int j2 = j | sd;
+                const uint64_t a = k[j], b = k[j2];
+                k[j] = fmin_bits(a, b);
+                k[j2] = fmax_bits(a, b);
+            }
+        } else {
+            const int m = sd >> 2;
+            const bool lower = (lid & (uint32_t)m) == 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint64_t y = xlane64(k[j], m);
+                k[j] = lower ? fmin_bits(k[j], y) : fmax_bits(k[j], y);
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ void cross_wave_step_f64(uint64_t (&k)[4], uint64_t *xk, uint32_t pw,
+                                                    bool mirror, bool lower) {
+    const uint32_t t = threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) xk[4 * t + j] = k[j];
+    __syncthreads();
+    const uint32_t l = __lane_id();
+    const uint32_t pt = pw * 64 + (mirror ? 63 - l : l);
+    uint64_t y[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) y[j] = xk[4 * pt + (mirror ? 3 - j : j)];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) k[j] = lower ? fmin_bits(k[j], y[j]) : fmax_bits(k[j], y[j]);
+}
+
 // Ascending sort of the workgroup's 256 NW elements (element i in thread
 // i / 4, slot i % 4).
 template <int NW, bool kLex>
@@ -237,12 +282,68 @@ __device__ __forceinline__ int mw_sort_chunk(uint32_t nc, char *smem, const Boun
     };
     load();
     for (uint32_t q = tid; q < kWCq; q += T) full[q] = 0;
+    bool sorted_packed = false;
+    if constexpr (NW == 2 && DPG_SORT_PACKED) {
+        // keys alone, packed as positive normal float64 (dpg_sortb.h
+        // sort_chunk): tag 01 | pid slot | top 45 - pkbits bits of the pair
+        // priority | the full partition key | position (9 bits); the keys
+        // and payloads are read back by position.  Pairs of one pid whose
+        // priorities agree in the kept bits may come out in pk order: the
+        // order is checked on (key, low pk bits) and, if broken, the chunk
+        // is sorted again the payload way below.  Partition keys over 29
+        // bits keep too few priority bits for this to pay.
+        const uint32_t pkb = f.pkbits;
+        if (pkb <= 29) {
+            const uint32_t ppb = min(32u, 45u - pkb);
+            const uint64_t pkm = (1ull << pkb) - 1ull;
+            uint64_t pk64[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t i = 4 * tid + j;
+                const uint64_t x = k[j];
+                const uint64_t pp = (x >> kSkPkBits) & 0xFFFFFFFFull;
+                const uint64_t pkfull = kWPk ? ((((uint64_t)x & kPkMask) << pksh) | (uint64_t)(o[j] >> PB))
+                                             : (x & pkm);
+                pk64[j] = i < nc ? (kSkTagF | ((x >> 56) << 54) | ((pp >> (32u - ppb)) << (9u + pkb)) |
+                                    (pkfull << 9) | (uint64_t)i)
+                                 : kSkPadF;
+            }
+            bitonic_sort_keys_f64<4>(pk64);
+            const uint32_t w = threadIdx.x >> 6;
+            cross_wave_step_f64(pk64, xk, w ^ 1u, true, (w & 1u) == 0);
+            half_clean_256_f64(pk64);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t pos = (uint32_t)pk64[j] & 511u;
+                const bool v = pk64[j] != kSkPadF;
+                k[j] = v ? ckey[pos] : kSkPad;
+                o[j] = v ? (kWPk ? (pos | ((uint32_t)cpkl[pos] << PB)) : cidx[pos]) : 0u;
+            }
+            __syncthreads();  // xk: the sort's exchange area, now each thread's last element
+            xk[tid] = k[3];
+            xo[tid] = o[3];
+            __syncthreads();
+            const uint64_t pk0 = tid ? xk[tid - 1] : 0ull;
+            const uint32_t po0 = tid ? xo[tid - 1] : 0u;
+            bool bad = false;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t i = 4 * tid + j;
+                const uint64_t pv = j ? k[j - 1] : pk0;
+                const uint32_t pvl = (j ? o[j - 1] : po0) >> PB;
+                const uint32_t lo = o[j] >> PB;
+                bad |= i > 0 && i < nc && (k[j] < pv || (kWPk && k[j] == pv && lo < pvl));
+            }
+            sorted_packed = __builtin_amdgcn_readfirstlane(mw_any<NW>(bad, scr) ? 0 : 1) != 0;
+            if (!sorted_packed) load();
+        }
+    }
     // by key only; wide partition keys (kWPk) whose low bits ride in the
     // payload re-sort by (key, payload) when two pairs of one pid share a
     // key (same priority and top 24 pk bits, ~2^-56 per pair of pairs):
     // the lexicographic comparator costs the common case a third more
-    mw_sort<NW, false>(k, o, xk, xo);
-    if constexpr (kWPk) {
+    if (!sorted_packed) mw_sort<NW, false>(k, o, xk, xo);
+    if (kWPk && !sorted_packed) {
         xk[tid] = k[3];
         xo[tid] = o[3];
         __syncthreads();

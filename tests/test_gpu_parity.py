@@ -585,3 +585,29 @@ def test_gpu_oversize_buckets_match_oracle(built, monkeypatch, name, kw, over):
     for k in ("sum", "nsum", "nsq"):
         if got[k] is not None:
             assert np.allclose(got[k], ref[k], rtol=1e-9, atol=1e-9), k
+
+
+def test_gpu_wide_packed_sort_and_its_fallback(built):
+    """The 2-wave sort kernel's float64-packed keys keep the top 45 - 24 =
+    21 bits of a pair priority at 24-bit partition keys: privacy ids of 300
+    pairs each (mpc 200: every record a candidate, so every chunk goes to
+    the 2-wave pass) collide in those bits in ~2 % of the ids, whose chunks
+    re-sort with full keys.  Partials equal the oracle's either way."""
+    rng = np.random.default_rng(2424)
+    P = 1 << 24
+    n_pid, per = 600, 300
+    pid = np.repeat(np.arange(n_pid), per)
+    pk = rng.integers(0, P, pid.size).astype(np.int64)
+    perm = rng.permutation(pid.size)
+    pid, pk = pid[perm].astype(np.int64), pk[perm]
+    val = rng.uniform(-2.0, 12.0, pid.size)
+    params = pdp.AggregateParams(metrics=[pdp.Metrics.COUNT, pdp.Metrics.SUM,
+                                          pdp.Metrics.PRIVACY_ID_COUNT],
+                                 max_partitions_contributed=200, max_contributions_per_partition=2,
+                                 min_value=0.0, max_value=10.0)
+    res, _ = run_engine(pid, pk, val, params, n_partitions=P)
+    ref = oracle.bound_aggregate(pid, pk, val, res.last_bound_fields, SEED)
+    got = {k: v.cpu().numpy() for k, v in res.last_partials.items() if v is not None}
+    assert np.array_equal(got["rows"], ref["rows"])
+    assert np.array_equal(got["count"], ref["count"])
+    assert np.allclose(got["sum"], ref["sum"], rtol=1e-9, atol=1e-9)
