@@ -1,12 +1,12 @@
 #!/bin/bash
-# Fusion bound: the bounding kernel's time per record
+# Fusion bound (tools/gpu_resident.sh): the bounding kernel's time per record
 # when its input -- the team level 2's output, written just before -- still
 # sits in the 256 MB Infinity Cache (N = 3e7 records of 8 bytes: 240 MB)
 # against inputs that cannot (1e8: 800 MB; 1e9: 8 GB), at config 2's 100
 # records per privacy id.  Same box, two runs each.
 set -o pipefail
 cd ${GRAFT_REPO_ROOT:-$(pwd)}
-T=r6q
+T=${TAG:-r6q}
 mkdir -p gpurun_out/$T
 for i in 1 2; do
 for w in "n3e7:30000000:300000" "n1e8:100000000:1000000" "n1e9:1000000000:10000000"; do
