@@ -101,7 +101,11 @@ constexpr int kRedoLevel2 = -100;
 #define DPG_PC_HALF 0
 #endif
 #ifndef DPG_IPT_PC
-#define DPG_IPT_PC 9  // records per thread of the histogram-free level 1 (10 spills: the spill reload waits for the run reservation right after issuing it)
+// records per thread of the histogram-free level 1: an even count, so that
+// the key columns load two records per 16-byte load (SrcSoAKey::fetch2);
+// same-box A/B at config 2: 9 records by 8-byte loads 6.38-6.40 ms, 8 by
+// pairs 5.97-5.99 (profiles/r6/r6w_pairs/); 10 exceeds the scatter's LDS
+#define DPG_IPT_PC 8
 #endif
 
 struct Buf {

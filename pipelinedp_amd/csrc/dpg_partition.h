@@ -213,6 +213,35 @@ struct SrcSoAKey {
         if (!pub) return true;
         return keep((uint32_t)a, pk[i]);
     }
+    // the scatter's pair view (piece mode): two consecutive records by one
+    // 16-byte load per column (8-byte aligned, any tile start), half the
+    // vector memory instructions of the 8-byte loads (DPG_L1_PAIRS; the
+    // scatter takes it with an even records-per-thread count)
+#ifndef DPG_L1_PAIRS
+#define DPG_L1_PAIRS 1
+#endif
+    static constexpr bool kFetchPairs = kFull && DPG_L1_PAIRS != 0;
+    __device__ __forceinline__ void fetch2(int64_t i, Raw &x0, Raw &x1) const {
+#if DPG_L1_NT
+        const u64x2a8 p = __builtin_nontemporal_load(reinterpret_cast<const u64x2a8 *>(pid + i));
+        const u64x2a8 q = __builtin_nontemporal_load(reinterpret_cast<const u64x2a8 *>(pk + i));
+#else
+        const u64x2a8 p = *reinterpret_cast<const u64x2a8 *>(pid + i);
+        const u64x2a8 q = *reinterpret_cast<const u64x2a8 *>(pk + i);
+#endif
+        if constexpr (kV) {
+#if DPG_L1_NT
+            const u64x2a8 v = __builtin_nontemporal_load(reinterpret_cast<const u64x2a8 *>(value + i));
+#else
+            const u64x2a8 v = *reinterpret_cast<const u64x2a8 *>(value + i);
+#endif
+            x0 = Raw{(PidW)p.x, (int64_t)q.x, __builtin_bit_cast(double, v.x)};
+            x1 = Raw{(PidW)p.y, (int64_t)q.y, __builtin_bit_cast(double, v.y)};
+        } else {
+            x0 = Raw{(PidW)p.x, (int64_t)q.x};
+            x1 = Raw{(PidW)p.y, (int64_t)q.y};
+        }
+    }
     // two consecutive records (i even) by 16-byte loads: the histogram pass
     // streams at the 16-B/lane rate instead of the 8-B one
     static constexpr bool kPairs = true;
