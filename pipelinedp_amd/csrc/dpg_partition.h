@@ -213,14 +213,15 @@ struct SrcSoAKey {
         if (!pub) return true;
         return keep((uint32_t)a, pk[i]);
     }
-    // the scatter's pair view (piece mode): two consecutive records by one
-    // 16-byte load per column (8-byte aligned, any tile start), half the
-    // vector memory instructions of the 8-byte loads (DPG_L1_PAIRS; the
-    // scatter takes it with an even records-per-thread count)
+    // the scatter's pair view: two consecutive records by one 16-byte load
+    // per column (8-byte aligned, any tile start), half the vector memory
+    // instructions of the 8-byte loads (DPG_L1_PAIRS; the scatter takes it
+    // with an even records-per-thread count: the piece mode and 12-byte
+    // records)
 #ifndef DPG_L1_PAIRS
 #define DPG_L1_PAIRS 1
 #endif
-    static constexpr bool kFetchPairs = kFull && DPG_L1_PAIRS != 0;
+    static constexpr bool kFetchPairs = DPG_L1_PAIRS != 0;
     __device__ __forceinline__ void fetch2(int64_t i, Raw &x0, Raw &x1) const {
 #if DPG_L1_NT
         const u64x2a8 p = __builtin_nontemporal_load(reinterpret_cast<const u64x2a8 *>(pid + i));
